@@ -1,0 +1,109 @@
+/*
+ * tonehip.h -- C ABI of libtonehip.so, the MI355X-native T-one streaming acoustic path.
+ *
+ * This is the boundary that replaces ONNX Runtime under tone/onnx_wrapper.py:
+ *
+ *   reference                                             | this library
+ *   ------------------------------------------------------+------------------------------------
+ *   ort.InferenceSession(model_path, providers=...)       | tone_session_create + tone_session_set_weight
+ *     (tone/onnx_wrapper.py:76-78)                        |   (one call per checkpoint tensor) + tone_session_finalize
+ *   ort_sess.run(None, {"signal": chunk, "state": state}) | tone_session_run
+ *     (tone/onnx_wrapper.py:123; I/O names and dims:      |   signal (B,2400,1) int32, state (B,219729) fp16
+ *      configs/streaming_acoustic/config.pbtxt:5-33)      |   -> logprobs (B,10,35) fp32, state_next (B,219729) fp16
+ *   Triton sequence batching with server-side state       | tone_session_run_slots (device-resident state slab,
+ *     (triton/model/config.pbtxt:26-69)                   |   stream slots gathered by index)
+ *
+ * All tensor arguments are DEVICE pointers (HIP global memory on the session's device); no torch
+ * types cross the boundary.  Every call is asynchronous on the given hipStream_t (passed as void*,
+ * NULL = the legacy default stream).  Functions return 0 on success or a negative TONE_E_* code;
+ * tone_last_error() returns a thread-local description of the last failure.
+ *
+ * A session is not re-entrant: serialize calls on one session (one session per GPU / per thread).
+ */
+#ifndef TONEHIP_H
+#define TONEHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TONE_ABI_VERSION 1
+
+/* boundary constants, tone/onnx_wrapper.py:30-34 */
+#define TONE_SAMPLE_RATE 8000
+#define TONE_AUDIO_CHUNK_SAMPLES 2400
+#define TONE_STATE_SIZE 219729
+#define TONE_FRAMES_PER_CHUNK 10
+#define TONE_VOCAB 35
+
+/* precision of the dense contractions; everything else (norms, softmax, log-softmax, state
+ * arithmetic) is fp32 in every mode, and the state is fp16 at the boundary. */
+#define TONE_PRECISION_FP32 0 /* fp32 MFMA (v_mfma_f32_32x32x2_f32), BASELINE config 2 */
+#define TONE_PRECISION_BF16 1 /* bf16 MFMA, fp32 accumulate, BASELINE config 3       */
+
+#define TONE_OK 0
+#define TONE_E_INVALID -1   /* bad argument (shape, null pointer, unknown name)       */
+#define TONE_E_STATE -2     /* call out of order (run before finalize, ...)          */
+#define TONE_E_HIP -3       /* a HIP runtime call failed                             */
+#define TONE_E_MISSING -4   /* finalize with checkpoint tensors missing              */
+
+typedef struct tone_session tone_session;
+
+int tone_abi_version(void);
+const char *tone_last_error(void);
+
+/* Create a session on `device` able to run batches of up to `max_batch` streams. */
+int tone_session_create(tone_session **out, int device, int precision, int max_batch);
+int tone_session_destroy(tone_session *s);
+
+/* Provide one checkpoint tensor by its reference state_dict name (tone/nn/model.py:39-41,
+ * e.g. "encoder.layers.3.feed_forward1.linear1.weight"; an HF "tone." prefix is accepted), as
+ * host fp32 data of exactly the reference shape's element count. */
+int tone_session_set_weight(tone_session *s, const char *name, const float *host_data, int64_t numel);
+
+/* Fold (RMSNorm gains into the following GEMM, BatchNorm into the preceding conv), pack
+ * (SwiGLU/GLU pairs interleaved, q|k|v concatenated) and upload the weights. */
+int tone_session_finalize(tone_session *s);
+
+/* Enable (1) / disable (0) hipGraph capture+replay of the per-step kernel sequence, keyed by
+ * (batch, I/O pointers).  Default 0. */
+int tone_session_set_graph(tone_session *s, int enable);
+
+/* One streaming step for `batch` independent streams.
+ *   signal      int32  [batch][2400]          PCM, int16 range (validated by the caller)
+ *   state_in    fp16   [batch][state_stride]  first 219729 elements are the flat state
+ *   logprobs    fp32   [batch][10][35]
+ *   state_out   fp16   [batch][state_stride]  must not alias state_in
+ * state_stride >= 219729 (elements). */
+int tone_session_run(tone_session *s, const int32_t *signal, const uint16_t *state_in, float *logprobs,
+                     uint16_t *state_out, int batch, int64_t state_stride, void *stream);
+
+/* Same step with the state in a device-resident slab of `n_slots` rows: stream i reads row
+ * slots[i] of slab_in and writes row slots[i] of slab_out (slot ids are device int32). */
+int tone_session_run_slots(tone_session *s, const int32_t *signal, const int32_t *slots, const uint16_t *slab_in,
+                           uint16_t *slab_out, int64_t slab_stride, float *logprobs, int batch, void *stream);
+
+/* Workspace bytes the session holds on the device (weights + activations). */
+int64_t tone_session_device_bytes(const tone_session *s);
+
+/* Average duration in microseconds of the named kernel family over the last timed run
+ * (see tone_session_set_timing); used by bench.py for the roofline figure. */
+int tone_session_set_timing(tone_session *s, int enable);
+double tone_session_kernel_us(const tone_session *s, const char *family, int64_t *launches);
+
+/* ---- diagnostics (parity localisation; not needed for serving) ------------------------------
+ * tone_session_debug_stop: end the step early -- stage 0 after the log-mel front end, 1 after the
+ * subsampling (pre-encode + out_norm), 2 + L after Conformer layer L (incl. reduction/upsampling
+ * at L = 6 / 14); -1 (default) runs the whole step.  Requires graph mode off.
+ * tone_session_debug_read: copy an internal fp32 activation buffer ("feats", "c1", "flat", "rA",
+ * "rB") of the last step to host memory. */
+int tone_session_debug_stop(tone_session *s, int stage);
+int tone_session_debug_read(tone_session *s, const char *buffer, void *host_dst, int64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TONEHIP_H */

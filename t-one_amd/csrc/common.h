@@ -1,0 +1,72 @@
+// Shared device helpers for the T-one HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+namespace tone {
+
+// ---- model constants (t-one_amd/config.py; tone/training/model_wrapper.py:27-115) -------------
+constexpr int kChunk = 2400;
+constexpr int kPreState = 80;
+constexpr int kWave = kChunk + kPreState;     // 2480 samples per mel pass
+constexpr int kMelT = 30;                     // mel frames per chunk
+constexpr int kWin = 160;
+constexpr int kHop = 80;
+constexpr int kBasisRows = 162;
+constexpr int kBins = 81;
+constexpr int kMels = 64;
+constexpr int kD = 384;
+constexpr int kHeads = 8;
+constexpr int kDk = 48;
+constexpr int kDff = 1536;
+constexpr int kRope = 32;
+constexpr int kConvK = 31;
+constexpr int kConvS = 30;
+constexpr int kMhsaS = 30;
+constexpr int kT = 10;                        // acoustic frames per chunk
+constexpr int kVocab = 35;
+constexpr int kSub1C = 32, kSub1Kt = 11, kSub1Kf = 21, kSub1F = 44, kSub1S = 10;
+constexpr int kSub2C = 64, kSub2Kt = 11, kSub2Kf = 11, kSub2F = 34, kSub2S = 8, kSub2Stride = 3;
+constexpr int kSub2In = kSub2S + kMelT;       // 38 time rows into conv2
+constexpr int kSubOut = kSub2C * kSub2F;      // 2176
+
+// flat state offsets (elements, per stream)
+constexpr int64_t kOffPre = 0;
+constexpr int64_t kOffMhsa = 80;
+constexpr int64_t kOffConv = 23120;
+constexpr int64_t kOffMhsaLen = 207440;
+constexpr int64_t kOffSub1 = 207441;
+constexpr int64_t kOffSub2 = 208081;
+constexpr int64_t kOffRed = 219345;
+constexpr int64_t kStateSize = 219729;
+
+constexpr float kRmsEps = 1e-8f;
+constexpr float kLnEps = 1e-5f;
+
+// Where stream b's state row lives: row b, or row slots[b] of a device-resident slab.
+struct StateRef {
+  const __half* in;
+  __half* out;
+  int64_t stride;          // elements between consecutive rows
+  const int* slots;        // nullptr -> identity
+  __device__ __forceinline__ int64_t row(int b) const { return (int64_t)(slots ? slots[b] : b) * stride; }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float round_h(float x) { return __half2float(__float2half_rn(x)); }
+
+}  // namespace tone

@@ -1,0 +1,768 @@
+// libtonehip.so: C ABI (include/tonehip.h), weight folding/packing and the per-step launch
+// sequence of the T-one streaming acoustic path.
+//
+// One step (Tone.forward_for_export, tone/nn/model.py:162-205) is a fixed sequence of ~200
+// kernel launches over a batch of independent streams; the activations of every stream are laid
+// out [stream * frames, 384] row-major so every pointwise projection is one GEMM with
+// M = batch * frames.  The step can be captured once per (batch, I/O pointers) into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/tonehip.h"
+#include "common.h"
+#include "kernels.h"
+
+using namespace tone;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) return fail(TONE_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct LayerW {
+  void* w13[2];       // [3072][384] SwiGLU-interleaved, norm folded
+  float* b13[2];
+  void* w2[2];        // [384][1536]
+  float* b2[2];
+  void* wqkv;         // recompute layers 0/7: [1152][384] folded; shared layers: [384][384] Wv folded
+  float* bqkv;
+  void* wq;           // layers 14/15: [384][384] unfolded
+  float* bq;
+  void* wkv;          // layers 14/15: [768][384] unfolded (k | v)
+  float* bkv;
+  float* norm_att;    // layers 14/15
+  float *qln_w, *qln_b, *kln_w, *kln_b;
+  void* wo;
+  float* bo;
+  void* wpw1;         // [768][384] GLU-interleaved, norm folded
+  float* bpw1;
+  float* wdw;         // [384][31] BN folded
+  float* bdw;
+  void* wpw2;
+  float* bpw2;
+  float* norm_out;
+};
+
+}  // namespace
+
+struct tone_session {
+  int device = 0;
+  int precision = TONE_PRECISION_FP32;
+  int max_batch = 0;
+  bool finalized = false;
+  bool use_graph = false;
+  bool timing = false;
+  int debug_stop = -1;
+  std::map<std::string, std::vector<float>> host;
+  std::vector<DevBuf> allocs;
+  int64_t dev_bytes = 0;
+
+  // weights
+  float *basis, *fbank, *rope_cos, *rope_sin;
+  float *pre_norm, *w1t, *scale1, *shift1, *w2c, *scale2, *shift2, *out_norm;
+  void* wsub_out;
+  float *wred, *bred, *bred_pw;
+  void* wred_pw;
+  float *whead, *bhead;
+  LayerW L[16];
+
+  // activations
+  float *feats, *c1, *flat, *rA, *rB, *h, *qkv, *xn, *kv, *kvp, *ctx, *g, *d, *probs, *yred;
+
+  // graphs
+  struct GraphKey {
+    int batch;
+    const void *a, *b, *c, *d, *e;
+    int64_t stride;
+    bool operator<(const GraphKey& o) const {
+      return std::memcmp(this, &o, sizeof(GraphKey)) < 0;
+    }
+  };
+  std::map<GraphKey, hipGraphExec_t> graphs;
+
+  // timing
+  struct Timed {
+    std::string family;
+    hipEvent_t a, b;
+  };
+  std::vector<Timed> timed;
+  size_t timed_used = 0;
+  std::map<std::string, std::pair<double, int64_t>> last_timing;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(tone_session* s, T** out, size_t count) {
+  void* p = nullptr;
+  const size_t bytes = count * sizeof(T);
+  HIP_TRY(hipMalloc(&p, bytes));
+  HIP_TRY(hipMemset(p, 0, bytes));
+  s->allocs.push_back({p, bytes});
+  s->dev_bytes += (int64_t)bytes;
+  *out = static_cast<T*>(p);
+  return TONE_OK;
+}
+
+int upload(tone_session* s, float** out, const std::vector<float>& v) {
+  int rc = dalloc(s, out, v.size());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(*out, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice));
+  return TONE_OK;
+}
+
+uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// GEMM weight in the session's precision (fp32, or bf16 bits)
+int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
+  if (s->precision == TONE_PRECISION_FP32) {
+    float* p;
+    int rc = upload(s, &p, v);
+    *out = p;
+    return rc;
+  }
+  std::vector<uint16_t> hb(v.size());
+  for (size_t i = 0; i < v.size(); ++i) hb[i] = f2bf(v[i]);
+  uint16_t* p;
+  int rc = dalloc(s, &p, hb.size());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(p, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+  *out = p;
+  return TONE_OK;
+}
+
+const std::vector<float>* getw(tone_session* s, const std::string& name, size_t numel, std::string* missing) {
+  auto it = s->host.find(name);
+  if (it == s->host.end() || it->second.size() != numel) {
+    if (missing->empty()) *missing = name;
+    return nullptr;
+  }
+  return &it->second;
+}
+
+// ---- front-end constants ----------------------------------------------------------------------
+// FilterbankFeatures._compute_forward_basis (feats.py:66-80): fft(eye(160)) rows 0..80 as
+// [Re ; Im], times the float32 symmetric Hann window, pre-emphasis matrix folded in, as float32.
+std::vector<float> make_basis() {
+  const int n = kWin;
+  std::vector<float> win(n);
+  const float step = (float)(M_PI * 2.0 / (double)(n - 1));
+  for (int k = 0; k < n; ++k) win[k] = 0.5f - 0.5f * std::cos((float)k * step);
+  std::vector<double> fb((size_t)n * kBasisRows);  // [k][r]
+  for (int k = 0; k < n; ++k)
+    for (int r = 0; r < kBasisRows; ++r) {
+      const int f = r < kBins ? r : r - kBins;
+      const double ang = -2.0 * M_PI * (double)((k * f) % n) / (double)n;
+      const double v = r < kBins ? std::cos(ang) : std::sin(ang);
+      fb[(size_t)k * kBasisRows + r] = v * (double)win[k];
+    }
+  const double pe = 0.97;
+  std::vector<float> basis((size_t)kBasisRows * n);
+  for (int k = 0; k < n; ++k)
+    for (int r = 0; r < kBasisRows; ++r) {
+      double v = fb[(size_t)k * kBasisRows + r];
+      if (k == 0) v = (1.0 - pe) * v;
+      if (k + 1 < n) v -= pe * fb[(size_t)(k + 1) * kBasisRows + r];
+      basis[(size_t)r * n + k] = (float)v;
+    }
+  return basis;
+}
+
+double hz_to_mel(double f) {
+  const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+  return f >= min_log_hz ? min_log_mel + std::log(f / min_log_hz) / logstep : f / f_sp;
+}
+
+// torchaudio 2.7.1 functional.melscale_fbanks(81, 0, 4000, 64, 8000, norm="slaney",
+// mel_scale="slaney") (called at feats.py:84-92), transposed to [64][81], float32 arithmetic.
+std::vector<float> make_fbank() {
+  const int nf = kBins, nm = kMels;
+  std::vector<float> freqs(nf), mpts(nm + 2), fpts(nm + 2);
+  for (int i = 0; i < nf; ++i) freqs[i] = (float)(4000.0 * i / (nf - 1));
+  const double m0 = hz_to_mel(0.0), m1 = hz_to_mel(4000.0);
+  const float f_sp = (float)(200.0 / 3), min_log_mel = (float)(1000.0 / (200.0 / 3));
+  const float logstep = (float)(std::log(6.4) / 27.0);
+  for (int i = 0; i < nm + 2; ++i) {
+    mpts[i] = (float)(m0 + (m1 - m0) * i / (nm + 1));
+    fpts[i] = mpts[i] >= min_log_mel ? 1000.0f * std::exp(logstep * (mpts[i] - min_log_mel)) : f_sp * mpts[i];
+  }
+  std::vector<float> fb((size_t)nm * nf);
+  for (int m = 0; m < nm; ++m) {
+    const float enorm = 2.0f / (fpts[m + 2] - fpts[m]);
+    for (int f = 0; f < nf; ++f) {
+      const float down = (-1.0f * (fpts[m] - freqs[f])) / (fpts[m + 1] - fpts[m]);
+      const float up = (fpts[m + 2] - freqs[f]) / (fpts[m + 2] - fpts[m + 1]);
+      fb[(size_t)m * nf + f] = std::fmax(0.0f, std::fmin(down, up)) * enorm;
+    }
+  }
+  return fb;
+}
+
+// RotaryPositionalEmbeddings._build_state (submodules.py:120-140), positions -30..9, 16 freqs.
+void make_rope(std::vector<float>& cs, std::vector<float>& sn) {
+  cs.resize(40 * 16);
+  sn.resize(40 * 16);
+  for (int j = 0; j < 16; ++j) {
+    const float e = (float)(2 * j) / 32.0f;
+    const float inv = 1.0f / std::pow(10000.0f, e);
+    for (int p = -30; p < 10; ++p) {
+      const float ang = (float)p * inv;
+      cs[(p + 30) * 16 + j] = std::cos(ang);
+      sn[(p + 30) * 16 + j] = std::sin(ang);
+    }
+  }
+}
+
+// ---- timing helpers ----------------------------------------------------------------------------
+struct Scope {
+  tone_session* s;
+  hipStream_t st;
+  size_t idx = (size_t)-1;
+  Scope(tone_session* s_, hipStream_t st_, const char* fam) : s(s_), st(st_) {
+    if (!s->timing) return;
+    if (s->timed_used == s->timed.size()) {
+      tone_session::Timed t;
+      t.family = fam;
+      (void)hipEventCreate(&t.a);
+      (void)hipEventCreate(&t.b);
+      s->timed.push_back(t);
+    }
+    idx = s->timed_used++;
+    s->timed[idx].family = fam;
+    (void)hipEventRecord(s->timed[idx].a, st);
+  }
+  ~Scope() {
+    if (idx != (size_t)-1) (void)hipEventRecord(s->timed[idx].b, st);
+  }
+};
+
+#define LAUNCH(fam, expr)                                                                      \
+  do {                                                                                         \
+    Scope _sc(s, st, fam);                                                                     \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) return fail(TONE_E_HIP, std::string(fam) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+int gemm_call(tone_session* s, hipStream_t st, const char* fam, const float* A, int64_t lda, const void* W, float* C,
+              int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
+              float alpha = 1.0f) {
+  GemmArgs a;
+  a.A = A;
+  a.lda = lda;
+  a.W = W;
+  a.C = C;
+  a.ldc = ldc;
+  a.bias = bias;
+  a.R = R;
+  a.ldr = ldc;
+  a.alpha = alpha;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.rowscale = rowscale;
+  a.inv_sqrt_k = (float)std::pow((double)K, -0.5);
+  LAUNCH(fam, gemm(a, epi, s->precision == TONE_PRECISION_BF16, st));
+  return TONE_OK;
+}
+
+#define CALL(x)          \
+  do {                   \
+    int _rc = (x);       \
+    if (_rc) return _rc; \
+  } while (0)
+
+// The whole streaming step (Tone.forward_for_export, model.py:162-205).
+int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* logp, int B, hipStream_t st) {
+  const int D = kD;
+  LAUNCH("mel", launch_mel(signal, sr, s->basis, s->fbank, s->feats, B, st));
+  if (s->debug_stop == 0) return TONE_OK;
+  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1t, s->scale1, s->shift1, s->c1, B, st));
+  LAUNCH("sub2", launch_sub2(s->c1, sr, s->w2c, s->scale2, s->shift2, s->flat, B, st));
+  CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * kT, D, kSubOut,
+                 EPI_STORE, 0));
+  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, st));
+  if (s->debug_stop == 1) return TONE_OK;
+  float* x = s->rA;
+  int T = kT;
+  for (int l = 0; l < 16; ++l) {
+    const LayerW& w = s->L[l];
+    const int M = B * T;
+    // FFN1 (conformer_blocks.py:812-814)
+    CALL(gemm_call(s, st, "gemm_ffn_up", x, D, w.w13[0], s->h, kDff, w.b13[0], M, 2 * kDff, D, EPI_SWIGLU, 1));
+    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[0], x, D, w.b2[0], M, D, kDff, EPI_RESID, 0, x, 0.5f));
+    // MHSA (conformer_blocks.py:816-825)
+    AttnArgs aa{};
+    aa.ctx = s->ctx;
+    aa.probs = s->probs;
+    aa.qln_w = w.qln_w;
+    aa.qln_b = w.qln_b;
+    aa.kln_w = w.kln_w;
+    aa.kln_b = w.kln_b;
+    aa.rope_cos = s->rope_cos;
+    aa.rope_sin = s->rope_sin;
+    aa.s = sr;
+    aa.T = T;
+    aa.B = B;
+    if (l < 14) {
+      const bool rec = (l == 0 || l == 7);
+      const int N = rec ? 3 * D : D;
+      CALL(gemm_call(s, st, "gemm_qkv", x, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1));
+      aa.S = 0;
+      aa.recompute = rec;
+      aa.reduced = 0;
+      if (rec) {
+        aa.q = s->qkv; aa.ldq = N;
+        aa.k = s->qkv + D; aa.ldk = N;
+        aa.v = s->qkv + 2 * D; aa.ldv = N;
+      } else {
+        aa.v = s->qkv; aa.ldv = D;
+      }
+    } else {
+      const int S = (l == 14) ? kMhsaS / 2 : kMhsaS;
+      LAUNCH("kv_assemble", launch_kv_assemble(x, w.norm_att, sr, l - 14, T, S, s->xn, s->kv, B, st));
+      CALL(gemm_call(s, st, "gemm_qkv", s->xn, D, w.wq, s->qkv, D, w.bq, M, D, D, EPI_STORE, 0));
+      CALL(gemm_call(s, st, "gemm_qkv", s->kv, D, w.wkv, s->kvp, 2 * D, w.bkv, B * (S + T), 2 * D, D, EPI_STORE, 0));
+      aa.S = S;
+      aa.recompute = 1;
+      aa.reduced = (l == 14);
+      aa.probs = nullptr;
+      aa.q = s->qkv; aa.ldq = D;
+      aa.k = s->kvp; aa.ldk = 2 * D;
+      aa.v = s->kvp + D; aa.ldv = 2 * D;
+    }
+    LAUNCH("attention", launch_attention(aa, st));
+    CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f));
+    // Convolution module (conformer_blocks.py:827-830)
+    CALL(gemm_call(s, st, "gemm_pw1", x, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1));
+    LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, T, B, st));
+    CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f));
+    // FFN2 + norm_out (conformer_blocks.py:832-836)
+    CALL(gemm_call(s, st, "gemm_ffn_up", x, D, w.w13[1], s->h, kDff, w.b13[1], M, 2 * kDff, D, EPI_SWIGLU, 1));
+    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[1], x, D, w.b2[1], M, D, kDff, EPI_RESID, 0, x, 0.5f));
+    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, st));
+    if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
+      LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, B, st));
+      CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * (kT / 2), D, 4 * D,
+                     EPI_STORE, 0));
+      x = s->rB;
+      T = kT / 2;
+    }
+    if (l == 14) {  // TemporalUpsampling (conformer.py:224-225)
+      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, st));
+      x = s->rA;
+      T = kT;
+    }
+    if (s->debug_stop == 2 + l) return TONE_OK;
+  }
+  LAUNCH("head", launch_head(s->rA, s->whead, s->bhead, logp, B * kT, st));
+  return TONE_OK;
+}
+
+int finalize_weights(tone_session* s) {
+  std::string miss;
+  const int D = kD;
+  auto W = [&](const std::string& n, size_t numel) { return getw(s, n, numel, &miss); };
+  const std::string pe = "encoder.pre_encode.";
+  auto pre_norm = W(pe + "pre_norm.weight", 64);
+  auto c1w = W(pe + "conv.0.0.weight", 32 * 231);
+  auto c1b = W(pe + "conv.0.0.bias", 32);
+  const std::vector<float>* bn1[4];
+  const std::vector<float>* bn2[4];
+  const char* bnn[4] = {"weight", "bias", "running_mean", "running_var"};
+  for (int i = 0; i < 4; ++i) {
+    bn1[i] = W(pe + "conv.0.1." + bnn[i], 32);
+    bn2[i] = W(pe + "conv.1.1." + bnn[i], 64);
+  }
+  auto c2w = W(pe + "conv.1.0.weight", (size_t)64 * 32 * 121);
+  auto c2b = W(pe + "conv.1.0.bias", 64);
+  auto outw = W(pe + "out.weight", (size_t)D * kSubOut);
+  auto outn = W(pe + "out_norm.weight", D);
+  const std::string tr = "encoder.temportal_reduction.";
+  auto rw = W(tr + "conv.weight", 4 * D * 3);
+  auto rb = W(tr + "conv.bias", 4 * D);
+  auto rpw = W(tr + "conv_pw.weight", (size_t)D * 4 * D);
+  auto rpb = W(tr + "conv_pw.bias", D);
+  auto hw = W("decoder.decoder_layers.0.weight", 35 * D);
+  auto hb = W("decoder.decoder_layers.0.bias", 35);
+  if (!miss.empty()) return fail(TONE_E_MISSING, "missing or mis-sized weight: " + miss);
+
+  CALL(upload(s, &s->basis, make_basis()));
+  CALL(upload(s, &s->fbank, make_fbank()));
+  std::vector<float> cs, sn;
+  make_rope(cs, sn);
+  CALL(upload(s, &s->rope_cos, cs));
+  CALL(upload(s, &s->rope_sin, sn));
+
+  CALL(upload(s, &s->pre_norm, *pre_norm));
+  {
+    std::vector<float> w1t(231 * 32), sc(32), sh(32);
+    for (int c = 0; c < 32; ++c)
+      for (int k = 0; k < 231; ++k) w1t[k * 32 + c] = (*c1w)[c * 231 + k];
+    for (int c = 0; c < 32; ++c) {
+      const double scale = (double)(*bn1[0])[c] / std::sqrt((double)(*bn1[3])[c] + 1e-5);
+      sc[c] = (float)scale;
+      sh[c] = (float)(((double)(*c1b)[c] - (double)(*bn1[2])[c]) * scale + (double)(*bn1[1])[c]);
+    }
+    CALL(upload(s, &s->w1t, w1t));
+    CALL(upload(s, &s->scale1, sc));
+    CALL(upload(s, &s->shift1, sh));
+  }
+  {
+    std::vector<float> sc(64), sh(64);
+    for (int c = 0; c < 64; ++c) {
+      const double scale = (double)(*bn2[0])[c] / std::sqrt((double)(*bn2[3])[c] + 1e-5);
+      sc[c] = (float)scale;
+      sh[c] = (float)(((double)(*c2b)[c] - (double)(*bn2[2])[c]) * scale + (double)(*bn2[1])[c]);
+    }
+    CALL(upload(s, &s->w2c, *c2w));
+    CALL(upload(s, &s->scale2, sc));
+    CALL(upload(s, &s->shift2, sh));
+  }
+  CALL(upload_w(s, &s->wsub_out, *outw));
+  CALL(upload(s, &s->out_norm, *outn));
+  CALL(upload(s, &s->wred, *rw));
+  CALL(upload(s, &s->bred, *rb));
+  CALL(upload_w(s, &s->wred_pw, *rpw));
+  CALL(upload(s, &s->bred_pw, *rpb));
+  CALL(upload(s, &s->whead, *hw));
+  CALL(upload(s, &s->bhead, *hb));
+
+  for (int l = 0; l < 16; ++l) {
+    const std::string p = "encoder.layers." + std::to_string(l) + ".";
+    LayerW& lw = s->L[l];
+    for (int f = 0; f < 2; ++f) {
+      const std::string ff = f == 0 ? "feed_forward1" : "feed_forward2";
+      auto nrm = W(p + "norm_" + ff + ".weight", D);
+      auto w1 = W(p + ff + ".linear1.weight", (size_t)kDff * D);
+      auto b1 = W(p + ff + ".linear1.bias", kDff);
+      auto wv = W(p + ff + ".linearv.weight", (size_t)kDff * D);
+      auto bv = W(p + ff + ".linearv.bias", kDff);
+      auto w2 = W(p + ff + ".linear2.weight", (size_t)D * kDff);
+      auto b2 = W(p + ff + ".linear2.bias", D);
+      if (!miss.empty()) return fail(TONE_E_MISSING, "missing or mis-sized weight: " + miss);
+      std::vector<float> w13((size_t)2 * kDff * D), b13(2 * kDff);
+      for (int q = 0; q < kDff / 32; ++q)
+        for (int r = 0; r < 32; ++r) {
+          const int src = 32 * q + r;
+          for (int k = 0; k < D; ++k) {
+            w13[(size_t)(64 * q + r) * D + k] = (*w1)[(size_t)src * D + k] * (*nrm)[k];
+            w13[(size_t)(64 * q + 32 + r) * D + k] = (*wv)[(size_t)src * D + k] * (*nrm)[k];
+          }
+          b13[64 * q + r] = (*b1)[src];
+          b13[64 * q + 32 + r] = (*bv)[src];
+        }
+      CALL(upload_w(s, &lw.w13[f], w13));
+      CALL(upload(s, &lw.b13[f], b13));
+      CALL(upload_w(s, &lw.w2[f], *w2));
+      CALL(upload(s, &lw.b2[f], *b2));
+    }
+    const std::string a = p + "self_attn.";
+    auto natt = W(p + "norm_self_att.weight", D);
+    auto wv = W(a + "linear_v.weight", (size_t)D * D);
+    auto bv = W(a + "linear_v.bias", D);
+    auto wo = W(a + "linear_out.weight", (size_t)D * D);
+    auto bo = W(a + "linear_out.bias", D);
+    if (!miss.empty()) return fail(TONE_E_MISSING, "missing or mis-sized weight: " + miss);
+    const bool rec = (l == 0 || l == 7 || l >= 14);
+    const std::vector<float>*wq = nullptr, *bq = nullptr, *wk = nullptr, *bk = nullptr;
+    if (rec) {
+      wq = W(a + "linear_q.weight", (size_t)D * D);
+      bq = W(a + "linear_q.bias", D);
+      wk = W(a + "linear_k.weight", (size_t)D * D);
+      bk = W(a + "linear_k.bias", D);
+      auto qw = W(a + "q_ln.weight", kDk), qb = W(a + "q_ln.bias", kDk);
+      auto kw = W(a + "k_ln.weight", kDk), kb = W(a + "k_ln.bias", kDk);
+      if (!miss.empty()) return fail(TONE_E_MISSING, "missing or mis-sized weight: " + miss);
+      CALL(upload(s, &lw.qln_w, *qw));
+      CALL(upload(s, &lw.qln_b, *qb));
+      CALL(upload(s, &lw.kln_w, *kw));
+      CALL(upload(s, &lw.kln_b, *kb));
+    }
+    if (l < 14) {
+      const int nb = rec ? 3 : 1;
+      std::vector<float> wqkv((size_t)nb * D * D), bqkv(nb * D);
+      const std::vector<float>* mats[3] = {wq, wk, wv};
+      const std::vector<float>* bias[3] = {bq, bk, bv};
+      for (int m = 0; m < nb; ++m) {
+        const int src = rec ? m : 2;
+        for (int n = 0; n < D; ++n) {
+          for (int k = 0; k < D; ++k) wqkv[(size_t)(m * D + n) * D + k] = (*mats[src])[(size_t)n * D + k] * (*natt)[k];
+          bqkv[m * D + n] = (*bias[src])[n];
+        }
+      }
+      CALL(upload_w(s, &lw.wqkv, wqkv));
+      CALL(upload(s, &lw.bqkv, bqkv));
+    } else {
+      std::vector<float> wkv((size_t)2 * D * D), bkv(2 * D);
+      std::memcpy(wkv.data(), wk->data(), (size_t)D * D * 4);
+      std::memcpy(wkv.data() + (size_t)D * D, wv->data(), (size_t)D * D * 4);
+      std::memcpy(bkv.data(), bk->data(), D * 4);
+      std::memcpy(bkv.data() + D, bv->data(), D * 4);
+      CALL(upload_w(s, &lw.wq, *wq));
+      CALL(upload(s, &lw.bq, *bq));
+      CALL(upload_w(s, &lw.wkv, wkv));
+      CALL(upload(s, &lw.bkv, bkv));
+      CALL(upload(s, &lw.norm_att, *natt));
+    }
+    CALL(upload_w(s, &lw.wo, *wo));
+    CALL(upload(s, &lw.bo, *bo));
+
+    const std::string c = p + "conv.";
+    auto ncv = W(p + "norm_conv.weight", D);
+    auto pw1 = W(c + "pointwise_conv1.weight", (size_t)2 * D * D);
+    auto pb1 = W(c + "pointwise_conv1.bias", 2 * D);
+    auto dww = W(c + "depthwise_conv.conv.weight", (size_t)D * kConvK);
+    auto dwb = W(c + "depthwise_conv.conv.bias", D);
+    const std::vector<float>* bn[4];
+    for (int i = 0; i < 4; ++i) bn[i] = W(c + "batch_norm." + bnn[i], D);
+    auto pw2 = W(c + "pointwise_conv2.weight", (size_t)D * D);
+    auto pb2 = W(c + "pointwise_conv2.bias", D);
+    auto nout = W(p + "norm_out.weight", D);
+    if (!miss.empty()) return fail(TONE_E_MISSING, "missing or mis-sized weight: " + miss);
+    std::vector<float> wp((size_t)2 * D * D), bp(2 * D);
+    for (int q = 0; q < D / 32; ++q)
+      for (int r = 0; r < 32; ++r) {
+        const int src = 32 * q + r;
+        for (int k = 0; k < D; ++k) {
+          wp[(size_t)(64 * q + r) * D + k] = (*pw1)[(size_t)src * D + k] * (*ncv)[k];
+          wp[(size_t)(64 * q + 32 + r) * D + k] = (*pw1)[(size_t)(D + src) * D + k] * (*ncv)[k];
+        }
+        bp[64 * q + r] = (*pb1)[src];
+        bp[64 * q + 32 + r] = (*pb1)[D + src];
+      }
+    CALL(upload_w(s, &lw.wpw1, wp));
+    CALL(upload(s, &lw.bpw1, bp));
+    std::vector<float> wd((size_t)D * kConvK), bd(D);
+    for (int ch = 0; ch < D; ++ch) {
+      const double scale = (double)(*bn[0])[ch] / std::sqrt((double)(*bn[3])[ch] + 1e-5);
+      for (int k = 0; k < kConvK; ++k) wd[(size_t)ch * kConvK + k] = (float)((double)(*dww)[(size_t)ch * kConvK + k] * scale);
+      bd[ch] = (float)(((double)(*dwb)[ch] - (double)(*bn[2])[ch]) * scale + (double)(*bn[1])[ch]);
+    }
+    CALL(upload(s, &lw.wdw, wd));
+    CALL(upload(s, &lw.bdw, bd));
+    CALL(upload_w(s, &lw.wpw2, *pw2));
+    CALL(upload(s, &lw.bpw2, *pb2));
+    CALL(upload(s, &lw.norm_out, *nout));
+  }
+
+  // activations
+  const size_t MB = (size_t)s->max_batch;
+  CALL(dalloc(s, &s->feats, MB * kMelT * kMels));
+  CALL(dalloc(s, &s->c1, MB * kSub1C * kMelT * kSub1F));
+  CALL(dalloc(s, &s->flat, MB * kT * kSubOut));
+  CALL(dalloc(s, &s->rA, MB * kT * D));
+  CALL(dalloc(s, &s->rB, MB * (kT / 2) * D));
+  CALL(dalloc(s, &s->h, MB * kT * kDff));
+  CALL(dalloc(s, &s->qkv, MB * kT * 3 * D));
+  CALL(dalloc(s, &s->xn, MB * kT * D));
+  CALL(dalloc(s, &s->kv, MB * 40 * D));
+  CALL(dalloc(s, &s->kvp, MB * 40 * 2 * D));
+  CALL(dalloc(s, &s->ctx, MB * kT * D));
+  CALL(dalloc(s, &s->g, MB * kT * D));
+  CALL(dalloc(s, &s->d, MB * kT * D));
+  CALL(dalloc(s, &s->probs, MB * kHeads * kT * 40));
+  CALL(dalloc(s, &s->yred, MB * (kT / 2) * 4 * D));
+  HIP_TRY(hipDeviceSynchronize());
+  return TONE_OK;
+}
+
+int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp, int batch, void* stream,
+               const void* key_a, const void* key_b) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  if (!s->finalized) return fail(TONE_E_STATE, "tone_session_finalize has not been called");
+  if (batch <= 0 || batch > s->max_batch)
+    return fail(TONE_E_INVALID, "batch " + std::to_string(batch) + " outside 1.." + std::to_string(s->max_batch));
+  if (!signal || !sr.in || !sr.out || !logp) return fail(TONE_E_INVALID, "null I/O pointer");
+  if (sr.stride < kStateSize) return fail(TONE_E_INVALID, "state stride < 219729");
+  if (sr.in == sr.out) return fail(TONE_E_INVALID, "state_out must not alias state_in");
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (s->use_graph && st != nullptr && !s->timing) {
+    tone_session::GraphKey k;
+    std::memset(&k, 0, sizeof(k));
+    k.batch = batch;
+    k.a = signal;
+    k.b = sr.in;
+    k.c = sr.out;
+    k.d = logp;
+    k.e = sr.slots;
+    k.stride = sr.stride;
+    (void)key_a;
+    (void)key_b;
+    auto it = s->graphs.find(k);
+    if (it == s->graphs.end()) {
+      HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      int rc = enqueue_step(s, signal, sr, logp, batch, st);
+      hipGraph_t graph = nullptr;
+      hipError_t e = hipStreamEndCapture(st, &graph);
+      if (rc) return rc;
+      if (e != hipSuccess) return fail(TONE_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+      hipGraphExec_t exec = nullptr;
+      HIP_TRY(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      HIP_TRY(hipGraphDestroy(graph));
+      it = s->graphs.emplace(k, exec).first;
+    }
+    HIP_TRY(hipGraphLaunch(it->second, st));
+    return TONE_OK;
+  }
+  return enqueue_step(s, signal, sr, logp, batch, st);
+}
+
+}  // namespace
+
+// =============================================================================================
+extern "C" {
+
+int tone_abi_version(void) { return TONE_ABI_VERSION; }
+
+const char* tone_last_error(void) { return g_err.c_str(); }
+
+int tone_session_create(tone_session** out, int device, int precision, int max_batch) {
+  if (!out) return fail(TONE_E_INVALID, "null out pointer");
+  if (precision != TONE_PRECISION_FP32 && precision != TONE_PRECISION_BF16)
+    return fail(TONE_E_INVALID, "unknown precision " + std::to_string(precision));
+  if (max_batch <= 0) return fail(TONE_E_INVALID, "max_batch must be positive");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(TONE_E_INVALID, "device " + std::to_string(device) + " not present");
+  HIP_TRY(hipSetDevice(device));
+  auto* s = new tone_session();
+  s->device = device;
+  s->precision = precision;
+  s->max_batch = max_batch;
+  *out = s;
+  return TONE_OK;
+}
+
+int tone_session_destroy(tone_session* s) {
+  if (!s) return TONE_OK;
+  (void)hipSetDevice(s->device);
+  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& t : s->timed) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  for (auto& a : s->allocs) (void)hipFree(a.p);
+  delete s;
+  return TONE_OK;
+}
+
+int tone_session_set_weight(tone_session* s, const char* name, const float* host_data, int64_t numel) {
+  if (!s || !name || !host_data || numel <= 0) return fail(TONE_E_INVALID, "bad set_weight arguments");
+  if (s->finalized) return fail(TONE_E_STATE, "session already finalized");
+  std::string n(name);
+  if (n.rfind("tone.", 0) == 0) n = n.substr(5);
+  s->host[n].assign(host_data, host_data + numel);
+  return TONE_OK;
+}
+
+int tone_session_finalize(tone_session* s) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  if (s->finalized) return TONE_OK;
+  HIP_TRY(hipSetDevice(s->device));
+  int rc = finalize_weights(s);
+  if (rc) return rc;
+  s->host.clear();
+  s->finalized = true;
+  return TONE_OK;
+}
+
+int tone_session_set_graph(tone_session* s, int enable) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  s->use_graph = enable != 0;
+  return TONE_OK;
+}
+
+int tone_session_run(tone_session* s, const int32_t* signal, const uint16_t* state_in, float* logprobs,
+                     uint16_t* state_out, int batch, int64_t state_stride, void* stream) {
+  StateRef sr{reinterpret_cast<const __half*>(state_in), reinterpret_cast<__half*>(state_out), state_stride, nullptr};
+  return run_common(s, signal, sr, logprobs, batch, stream, nullptr, nullptr);
+}
+
+int tone_session_run_slots(tone_session* s, const int32_t* signal, const int32_t* slots, const uint16_t* slab_in,
+                           uint16_t* slab_out, int64_t slab_stride, float* logprobs, int batch, void* stream) {
+  if (!slots) return fail(TONE_E_INVALID, "null slots");
+  StateRef sr{reinterpret_cast<const __half*>(slab_in), reinterpret_cast<__half*>(slab_out), slab_stride, slots};
+  return run_common(s, signal, sr, logprobs, batch, stream, nullptr, nullptr);
+}
+
+int64_t tone_session_device_bytes(const tone_session* s) { return s ? s->dev_bytes : 0; }
+
+int tone_session_debug_stop(tone_session* s, int stage) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  s->debug_stop = stage;
+  return TONE_OK;
+}
+
+int tone_session_debug_read(tone_session* s, const char* buffer, void* host_dst, int64_t bytes) {
+  if (!s || !buffer || !host_dst || bytes < 0) return fail(TONE_E_INVALID, "bad debug_read arguments");
+  if (!s->finalized) return fail(TONE_E_STATE, "session not finalized");
+  const size_t MB = (size_t)s->max_batch;
+  const std::string n(buffer);
+  const float* p = nullptr;
+  size_t cap = 0;
+  if (n == "feats") { p = s->feats; cap = MB * kMelT * kMels; }
+  else if (n == "c1") { p = s->c1; cap = MB * kSub1C * kMelT * kSub1F; }
+  else if (n == "flat") { p = s->flat; cap = MB * kT * kSubOut; }
+  else if (n == "rA") { p = s->rA; cap = MB * kT * kD; }
+  else if (n == "rB") { p = s->rB; cap = MB * (kT / 2) * kD; }
+  else return fail(TONE_E_INVALID, "unknown debug buffer " + n);
+  if ((size_t)bytes > cap * sizeof(float)) return fail(TONE_E_INVALID, "debug_read larger than the buffer");
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(host_dst, p, (size_t)bytes, hipMemcpyDeviceToHost));
+  return TONE_OK;
+}
+
+int tone_session_set_timing(tone_session* s, int enable) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  s->timing = enable != 0;
+  s->timed_used = 0;
+  return TONE_OK;
+}
+
+double tone_session_kernel_us(const tone_session* cs, const char* family, int64_t* launches) {
+  auto* s = const_cast<tone_session*>(cs);
+  if (!s || !family) return -1.0;
+  double tot = 0.0;
+  int64_t n = 0;
+  for (size_t i = 0; i < s->timed_used; ++i) {
+    if (s->timed[i].family != family) continue;
+    if (hipEventSynchronize(s->timed[i].b) != hipSuccess) return -1.0;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->timed[i].a, s->timed[i].b) != hipSuccess) return -1.0;
+    tot += ms * 1000.0;
+    ++n;
+  }
+  if (launches) *launches = n;
+  return n ? tot / n : 0.0;
+}
+
+}  // extern "C"

@@ -1,0 +1,254 @@
+"""Host side of the acoustic path: the drop-in ``StreamingCTCModel`` and the device ``ToneSession``.
+
+``StreamingCTCModel`` mirrors ``tone.onnx_wrapper.StreamingCTCModel`` (tone/onnx_wrapper.py:17-123):
+same class constants, factories, ``forward(audio_chunk, state=None)`` signature, numpy I/O, and
+the same exceptions for bad inputs, so ``tone.pipeline.StreamingCTCPipeline`` (which reads the
+constants from the class and calls ``model.forward``, tone/pipeline.py:49,141-147) runs unchanged
+with it.  Instead of ``ort.InferenceSession.run`` it calls ``libtonehip.so``.
+
+``ToneSession`` is the high-throughput interface: torch device tensors in and out, optional
+hipGraph replay, and a slot API over a device-resident state slab.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+import numpy.typing as npt
+
+from . import _lib
+from . import config as C
+from .weights import load_weights, synthetic_weights
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class ToneSession:
+    """One libtonehip session on one GPU: folded weights + activations resident in HBM."""
+
+    def __init__(self, weights: dict, device: int = 0, precision: str = "fp32", max_batch: int = 256,
+                 graph: bool = False):
+        torch = _torch()
+        lib = _lib.load()
+        if precision not in _lib.PRECISION:
+            raise ValueError(f"precision must be one of {sorted(_lib.PRECISION)}, got {precision!r}")
+        if not torch.cuda.is_available():
+            raise RuntimeError("ToneSession needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = int(device)
+        self.precision = precision
+        self.max_batch = int(max_batch)
+        self._lib = lib
+        h = ctypes.c_void_p()
+        torch.cuda.set_device(self.device)
+        _lib.check(lib.tone_session_create(ctypes.byref(h), self.device, _lib.PRECISION[precision], self.max_batch),
+                   "tone_session_create")
+        self._h = h
+        for name, arr in weights.items():
+            a = np.ascontiguousarray(arr, dtype=np.float32)
+            _lib.check(lib.tone_session_set_weight(h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), a.size),
+                       f"tone_session_set_weight({name})")
+        _lib.check(lib.tone_session_finalize(h), "tone_session_finalize")
+        if graph:
+            _lib.check(lib.tone_session_set_graph(h, 1), "tone_session_set_graph")
+        self.dev = torch.device("cuda", self.device)
+
+    # --- raw device-pointer step --------------------------------------------------------------
+    def run(self, signal, state_in, logprobs, state_out, stream=None) -> None:
+        """signal int32 (B,2400[,1]), state_in/state_out fp16 (B, >=219729), logprobs fp32 (B,10,35);
+        all contiguous torch tensors on this session's device."""
+        torch = _torch()
+        b = int(signal.shape[0])
+        for t, dt in ((signal, torch.int32), (state_in, torch.float16), (state_out, torch.float16),
+                      (logprobs, torch.float32)):
+            if t.dtype != dt or t.device != self.dev:
+                raise ValueError(f"expected {dt} tensor on {self.dev}, got {t.dtype} on {t.device}")
+        if state_in.stride(1) != 1 or state_out.stride(1) != 1 or state_in.stride(0) != state_out.stride(0):
+            raise ValueError("state tensors must be row-contiguous with equal row strides")
+        if not signal.is_contiguous() or not logprobs.is_contiguous():
+            raise ValueError("signal and logprobs must be contiguous")
+        st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
+        _lib.check(self._lib.tone_session_run(self._h, signal.data_ptr(), state_in.data_ptr(), logprobs.data_ptr(),
+                                              state_out.data_ptr(), b, state_in.stride(0), st),
+                   "tone_session_run")
+
+    def run_slots(self, signal, slots, slab_in, slab_out, logprobs, stream=None) -> None:
+        """Stream i uses row slots[i] of the device-resident state slabs (int32 slot ids)."""
+        torch = _torch()
+        st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
+        _lib.check(self._lib.tone_session_run_slots(self._h, signal.data_ptr(), slots.data_ptr(), slab_in.data_ptr(),
+                                                    slab_out.data_ptr(), slab_in.stride(0), logprobs.data_ptr(),
+                                                    int(signal.shape[0]), st),
+                   "tone_session_run_slots")
+
+    def step(self, signal, state=None):
+        """Allocate-and-run convenience: returns (logprobs, next_state) device tensors."""
+        torch = _torch()
+        b = int(signal.shape[0])
+        if state is None:
+            state = torch.zeros((b, C.STATE_SIZE), dtype=torch.float16, device=self.dev)
+        out_state = torch.empty_like(state)
+        logp = torch.empty((b, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=self.dev)
+        self.run(signal.contiguous(), state, logp, out_state)
+        return logp, out_state
+
+    # --- timing (bench.py) --------------------------------------------------------------------
+    def set_timing(self, enable: bool) -> None:
+        _lib.check(self._lib.tone_session_set_timing(self._h, int(enable)), "tone_session_set_timing")
+
+    def kernel_us(self, family: str) -> tuple[float, int]:
+        n = ctypes.c_int64(0)
+        us = self._lib.tone_session_kernel_us(self._h, family.encode(), ctypes.byref(n))
+        return float(us), int(n.value)
+
+    def set_graph(self, enable: bool) -> None:
+        _lib.check(self._lib.tone_session_set_graph(self._h, int(enable)), "tone_session_set_graph")
+
+    def debug_stop(self, stage: int) -> None:
+        _lib.check(self._lib.tone_session_debug_stop(self._h, int(stage)), "tone_session_debug_stop")
+
+    def debug_read(self, name: str, shape) -> np.ndarray:
+        out = np.empty(shape, np.float32)
+        _lib.check(self._lib.tone_session_debug_read(self._h, name.encode(), out.ctypes.data_as(ctypes.c_void_p),
+                                                     out.nbytes), f"tone_session_debug_read({name})")
+        return out
+
+    @property
+    def device_bytes(self) -> int:
+        return int(self._lib.tone_session_device_bytes(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.tone_session_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def validate_inputs(audio_chunk, state):
+    """Input checks of tone/onnx_wrapper.py:100-121 (same exception types); returns the state,
+    zero-initialised when None (onnx_wrapper.py:114-115)."""
+    if not isinstance(audio_chunk, np.ndarray):
+        raise TypeError(f"Incorrect 'audio_chunk' type: expected np.ndarray, but got {type(audio_chunk)}")
+    if audio_chunk.ndim != 3 or audio_chunk.shape[1:] != (C.AUDIO_CHUNK_SAMPLES, 1):
+        raise ValueError(
+            f"Shape of 'audio_chunk' must be (B, {C.AUDIO_CHUNK_SAMPLES}, 1), but got {audio_chunk.shape}",
+        )
+    if audio_chunk.dtype != np.int32:
+        raise ValueError(f"Incorrect dtype of 'audio_chunk': expected np.int32, but got {audio_chunk.dtype}")
+    if audio_chunk.size and (audio_chunk.min() < -32768 or audio_chunk.max() > 32767):
+        raise ValueError(
+            "Samples in 'audio_chunk' must be in range [-32768; 32767], "
+            f"but it is in range [{audio_chunk.min()}; {audio_chunk.max()}]",
+        )
+    batch_size = audio_chunk.shape[0]
+    if state is None:
+        state = np.zeros((batch_size, C.STATE_SIZE), dtype=np.float16)
+    if not isinstance(state, np.ndarray):
+        raise TypeError(f"Incorrect 'state' type: expected np.ndarray or None, but got {type(state)}")
+    if state.shape != (batch_size, C.STATE_SIZE):
+        raise ValueError(f"Shape of 'state' must be ({batch_size}, {C.STATE_SIZE}), but got {state.shape}")
+    if state.dtype != np.float16:
+        raise ValueError(f"Incorrect dtype of 'state': expected np.float16, but got {state.dtype}")
+    return state
+
+
+class StreamingCTCModel:
+    """Drop-in for ``tone.onnx_wrapper.StreamingCTCModel`` running on an MI355X GPU.
+
+    Class constants are identical to tone/onnx_wrapper.py:30-34 (the pipeline reads them from the
+    class, tone/pipeline.py:49,141,154,161).
+    """
+
+    InputType = npt.NDArray[np.int32]
+    OutputType = npt.NDArray[np.float32]
+    StateType = npt.NDArray[np.float16]
+
+    SAMPLE_RATE = C.SAMPLE_RATE
+    MEAN_TIME_BIAS = C.MEAN_TIME_BIAS
+    AUDIO_CHUNK_SAMPLES = C.AUDIO_CHUNK_SAMPLES
+    FRAME_SIZE = C.FRAME_SIZE
+    STATE_SIZE = C.STATE_SIZE
+
+    HF_REPO = "t-tech/T-one"
+    HF_WEIGHTS = "model.safetensors"
+
+    @classmethod
+    def from_hugging_face(cls) -> "StreamingCTCModel":
+        """tone/onnx_wrapper.py:38-50 -- resolves the checkpoint through the HF cache."""
+        return cls.from_local(cls.download_from_hugging_face())
+
+    @classmethod
+    def download_from_hugging_face(cls) -> str:
+        """tone/onnx_wrapper.py:52-63, but fetching the torch checkpoint (this path does not run
+        ONNX graphs).  Works offline when the file is already in the HF cache."""
+        from huggingface_hub import hf_hub_download
+        return hf_hub_download(cls.HF_REPO, cls.HF_WEIGHTS)
+
+    @classmethod
+    def from_local(cls, model_path: str | Path, providers: Optional[list[str]] = None, *, device: int = 0,
+                   precision: str = "fp32", max_batch: int = 64) -> "StreamingCTCModel":
+        """tone/onnx_wrapper.py:65-78.  ``model_path``: model.safetensors / weights.npz / torch
+        state_dict (.pt, weights_only) or a directory holding one.  ``providers`` is accepted for
+        signature compatibility; the MI355X device is chosen with ``device``."""
+        del providers
+        return cls(ToneSession(load_weights(model_path), device=device, precision=precision, max_batch=max_batch))
+
+    @classmethod
+    def from_synthetic(cls, seed: int = 0, **kw) -> "StreamingCTCModel":
+        """Random-init weights of the T-one architecture (tests / benchmarks; no checkpoint offline)."""
+        return cls(ToneSession(synthetic_weights(seed), **kw))
+
+    def __init__(self, session: ToneSession) -> None:
+        self._sess = session
+        self._buffers: dict = {}
+
+    @property
+    def session(self) -> ToneSession:
+        return self._sess
+
+    def _io(self, b: int):
+        torch = _torch()
+        if b not in self._buffers:
+            dev = self._sess.dev
+            self._buffers[b] = (
+                torch.empty((b, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32, device=dev),
+                torch.empty((b, C.STATE_SIZE), dtype=torch.float16, device=dev),
+                torch.empty((b, C.STATE_SIZE), dtype=torch.float16, device=dev),
+                torch.empty((b, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev),
+            )
+        return self._buffers[b]
+
+    def forward(self, audio_chunk: InputType, state: StateType | None = None) -> tuple[OutputType, StateType]:
+        """Run the acoustic model on a batch of chunks (tone/onnx_wrapper.py:84-123).
+
+        Returns logprobs (B, 10, 35) float32 and the next state (B, 219729) float16.
+        """
+        state = validate_inputs(audio_chunk, state)
+        batch_size = audio_chunk.shape[0]
+
+        torch = _torch()
+        if batch_size == 0:
+            return (np.zeros((0, C.CHUNK_FRAMES, C.VOCAB), np.float32), np.zeros((0, C.STATE_SIZE), np.float16))
+        outs_l, outs_s = [], []
+        for s0 in range(0, batch_size, self._sess.max_batch):
+            s1 = min(batch_size, s0 + self._sess.max_batch)
+            b = s1 - s0
+            sig, st_in, st_out, logp = self._io(b)
+            sig.copy_(torch.from_numpy(np.ascontiguousarray(audio_chunk[s0:s1, :, 0])))
+            st_in.copy_(torch.from_numpy(np.ascontiguousarray(state[s0:s1])))
+            self._sess.run(sig, st_in, logp, st_out)
+            outs_l.append(logp.cpu().numpy())
+            outs_s.append(st_out.cpu().numpy())
+        logprobs = outs_l[0] if len(outs_l) == 1 else np.concatenate(outs_l)
+        next_state = outs_s[0] if len(outs_s) == 1 else np.concatenate(outs_s)
+        return logprobs, next_state

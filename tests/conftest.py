@@ -1,0 +1,12 @@
+"""Test configuration: the ``gpu`` marker and import paths (repo root for ``tone_amd``, oracle/)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built libtonehip.so")
