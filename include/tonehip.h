@@ -97,7 +97,7 @@ double tone_session_kernel_us(const tone_session *s, const char *family, int64_t
  * tone_session_debug_stop: end the step early -- stage 0 after the log-mel front end, 1 after the
  * subsampling (pre-encode + out_norm), 2 + L after Conformer layer L (incl. reduction/upsampling
  * at L = 6 / 14); -1 (default) runs the whole step.  Requires graph mode off.
- * tone_session_debug_read: copy an internal fp32 activation buffer ("feats", "c1", "flat", "rA",
+ * tone_session_debug_read: copy an internal fp32 activation buffer ("feats", "x2", "flat", "rA",
  * "rB") of the last step to host memory. */
 int tone_session_debug_stop(tone_session *s, int stage);
 int tone_session_debug_read(tone_session *s, const char *buffer, void *host_dst, int64_t bytes);

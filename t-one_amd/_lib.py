@@ -47,6 +47,10 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # torch bundles its own libamdhip64.so.7; importing it first makes libtonehip bind to that same
+    # HIP runtime (same SONAME), so torch-allocated device pointers and our kernels share one
+    # runtime instance in the process.
+    import torch  # noqa: F401
     if not LIB_PATH.exists():
         raise ImportError(
             f"{LIB_PATH} not found: build it with `make -C t-one_amd/csrc` or __graft_entry__.build(). "

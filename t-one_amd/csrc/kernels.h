@@ -9,7 +9,7 @@
 
 namespace tone {
 
-enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GLU = 3 };
+enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GLU = 3, EPI_CONV2 = 4 };
 
 struct GemmArgs {
   const float* A;
@@ -24,21 +24,31 @@ struct GemmArgs {
   int M, N, K;
   int rowscale;       // 1: divide each row by ||a_row||/sqrt(K) + 1e-8 (folded RMSNorm)
   float inv_sqrt_k;
+  // split-K workspace (nullptr disables split-K)
+  float* ws;          // [nsplit][M][N] fp32 partials
+  float* ws_ss;       // [nsplit][M] partial row sums of squares (rowscale)
+  int64_t ws_cap;     // floats available in ws
+  int k_split;        // set by the launcher
+  const float* scale; // EPI_CONV2: folded BatchNorm scale per output channel (bias = shift)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
+
+// a3 conv2 as an implicit GEMM over all streams: A rows gathered from the channels-last
+// [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,
+// epilogue SiLU(acc*scale + shift) -> flat [B*10][34*64] (f-major, channel-minor).
+hipError_t conv2_gemm(const float* x2, const void* w, const float* scale, const float* shift, float* flat, int B,
+                      bool bf16, hipStream_t st);
 
 // a1/a2: PCM -> fp16 -> log-mel fp16 features [B][30][64] (stored as fp32 values); preproc state
 // and mhsa_len of the next state.
 hipError_t launch_mel(const int32_t* pcm, StateRef s, const float* basis, const float* fbank, float* feats, int B,
                       hipStream_t st);
 
-// a3 part 1: pre-norm RMSNorm(64) + sub1 state + Conv2d(1->32,k11x21) + BN + SiLU -> c1 [B][32][30][44]
-hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1t, const float* scale1,
-                       const float* shift1, float* c1, int B, hipStream_t st);
-// a3 part 2: sub2 state + Conv2d(32->64,k11x11,s(3,1)) + BN + SiLU -> flat [B][10][64*34]
-hipError_t launch_sub2(const float* c1, StateRef s, const float* w2, const float* scale2, const float* shift2,
-                       float* flat, int B, hipStream_t st);
+// a3 part 1: pre-norm RMSNorm(64) + sub1 state + Conv2d(1->32,k11x21) + BN + SiLU, written with the
+// carried sub2 rows as the channels-last conv2 input x2 [B][38][44][32]; next sub1/sub2 states.
+hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const float* scale1,
+                       const float* shift1, float* x2, int B, hipStream_t st);
 
 // In-place RMSNorm over rows of 384 (norm_out, out_norm).
 hipError_t launch_rmsnorm(float* x, const float* w, int rows, hipStream_t st);

@@ -80,7 +80,8 @@ struct tone_session {
 
   // weights
   float *basis, *fbank, *rope_cos, *rope_sin;
-  float *pre_norm, *w1t, *scale1, *shift1, *w2c, *scale2, *shift2, *out_norm;
+  float *pre_norm, *w1, *scale1, *shift1, *scale2, *shift2, *out_norm;
+  void* w2c;
   void* wsub_out;
   float *wred, *bred, *bred_pw;
   void* wred_pw;
@@ -88,7 +89,9 @@ struct tone_session {
   LayerW L[16];
 
   // activations
-  float *feats, *c1, *flat, *rA, *rB, *h, *qkv, *xn, *kv, *kvp, *ctx, *g, *d, *probs, *yred;
+  float *feats, *x2, *flat, *rA, *rB, *h, *qkv, *xn, *kv, *kvp, *ctx, *g, *d, *probs, *yred;
+  float *ws, *ws_ss;
+  int64_t ws_cap = 0;
 
   // graphs
   struct GraphKey {
@@ -288,6 +291,10 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const float* A, 
   a.K = K;
   a.rowscale = rowscale;
   a.inv_sqrt_k = (float)std::pow((double)K, -0.5);
+  a.ws = s->ws;
+  a.ws_ss = s->ws_ss;
+  a.ws_cap = s->ws_cap;
+  a.k_split = 0;
   LAUNCH(fam, gemm(a, epi, s->precision == TONE_PRECISION_BF16, st));
   return TONE_OK;
 }
@@ -303,8 +310,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   const int D = kD;
   LAUNCH("mel", launch_mel(signal, sr, s->basis, s->fbank, s->feats, B, st));
   if (s->debug_stop == 0) return TONE_OK;
-  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1t, s->scale1, s->shift1, s->c1, B, st));
-  LAUNCH("sub2", launch_sub2(s->c1, sr, s->w2c, s->scale2, s->shift2, s->flat, B, st));
+  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->scale1, s->shift1, s->x2, B, st));
+  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, s->precision == TONE_PRECISION_BF16, st));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * kT, D, kSubOut,
                  EPI_STORE, 0));
   LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, st));
@@ -422,15 +429,13 @@ int finalize_weights(tone_session* s) {
 
   CALL(upload(s, &s->pre_norm, *pre_norm));
   {
-    std::vector<float> w1t(231 * 32), sc(32), sh(32);
-    for (int c = 0; c < 32; ++c)
-      for (int k = 0; k < 231; ++k) w1t[k * 32 + c] = (*c1w)[c * 231 + k];
+    std::vector<float> sc(32), sh(32);
     for (int c = 0; c < 32; ++c) {
       const double scale = (double)(*bn1[0])[c] / std::sqrt((double)(*bn1[3])[c] + 1e-5);
       sc[c] = (float)scale;
       sh[c] = (float)(((double)(*c1b)[c] - (double)(*bn1[2])[c]) * scale + (double)(*bn1[1])[c]);
     }
-    CALL(upload(s, &s->w1t, w1t));
+    CALL(upload(s, &s->w1, *c1w));
     CALL(upload(s, &s->scale1, sc));
     CALL(upload(s, &s->shift1, sh));
   }
@@ -441,11 +446,22 @@ int finalize_weights(tone_session* s) {
       sc[c] = (float)scale;
       sh[c] = (float)(((double)(*c2b)[c] - (double)(*bn2[2])[c]) * scale + (double)(*bn2[1])[c]);
     }
-    CALL(upload(s, &s->w2c, *c2w));
+    // conv2 weight tap-major [c2][kt][kf][ci] for the implicit GEMM over channels-last input
+    std::vector<float> w2r((size_t)64 * 121 * 32);
+    for (int c2 = 0; c2 < 64; ++c2)
+      for (int ci = 0; ci < 32; ++ci)
+        for (int k = 0; k < 121; ++k) w2r[((size_t)c2 * 121 + k) * 32 + ci] = (*c2w)[((size_t)c2 * 32 + ci) * 121 + k];
+    CALL(upload_w(s, &s->w2c, w2r));
     CALL(upload(s, &s->scale2, sc));
     CALL(upload(s, &s->shift2, sh));
   }
-  CALL(upload_w(s, &s->wsub_out, *outw));
+  {  // out Linear columns permuted from c*34+f to f*64+c (the conv2 GEMM writes channel-minor rows)
+    std::vector<float> wo((size_t)D * kSubOut);
+    for (int n = 0; n < D; ++n)
+      for (int c = 0; c < 64; ++c)
+        for (int f = 0; f < 34; ++f) wo[(size_t)n * kSubOut + f * 64 + c] = (*outw)[(size_t)n * kSubOut + c * 34 + f];
+    CALL(upload_w(s, &s->wsub_out, wo));
+  }
   CALL(upload(s, &s->out_norm, *outn));
   CALL(upload(s, &s->wred, *rw));
   CALL(upload(s, &s->bred, *rb));
@@ -575,7 +591,7 @@ int finalize_weights(tone_session* s) {
   // activations
   const size_t MB = (size_t)s->max_batch;
   CALL(dalloc(s, &s->feats, MB * kMelT * kMels));
-  CALL(dalloc(s, &s->c1, MB * kSub1C * kMelT * kSub1F));
+  CALL(dalloc(s, &s->x2, MB * kSub2In * kSub1F * kSub1C));
   CALL(dalloc(s, &s->flat, MB * kT * kSubOut));
   CALL(dalloc(s, &s->rA, MB * kT * D));
   CALL(dalloc(s, &s->rB, MB * (kT / 2) * D));
@@ -589,6 +605,10 @@ int finalize_weights(tone_session* s) {
   CALL(dalloc(s, &s->d, MB * kT * D));
   CALL(dalloc(s, &s->probs, MB * kHeads * kT * 40));
   CALL(dalloc(s, &s->yred, MB * (kT / 2) * 4 * D));
+  // split-K workspace: only small batches split (large ones fill the chip with whole-K tiles)
+  s->ws_cap = 16ll << 20;
+  CALL(dalloc(s, &s->ws, (size_t)s->ws_cap));
+  CALL(dalloc(s, &s->ws_ss, (size_t)16 * MB * 40));
   HIP_TRY(hipDeviceSynchronize());
   return TONE_OK;
 }
@@ -729,7 +749,7 @@ int tone_session_debug_read(tone_session* s, const char* buffer, void* host_dst,
   const float* p = nullptr;
   size_t cap = 0;
   if (n == "feats") { p = s->feats; cap = MB * kMelT * kMels; }
-  else if (n == "c1") { p = s->c1; cap = MB * kSub1C * kMelT * kSub1F; }
+  else if (n == "x2") { p = s->x2; cap = MB * kSub2In * kSub1F * kSub1C; }
   else if (n == "flat") { p = s->flat; cap = MB * kT * kSubOut; }
   else if (n == "rA") { p = s->rA; cap = MB * kT * kD; }
   else if (n == "rB") { p = s->rB; cap = MB * (kT / 2) * kD; }

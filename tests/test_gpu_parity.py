@@ -214,8 +214,9 @@ def test_numpy_dropin_matches_session(weights):
     assert st.shape == (6, C.STATE_SIZE) and st.dtype == np.float16
     lp2, st2 = model.forward(chunk, st)
     s = model.session
-    ref, _ = gpu_step(s, chunk[:, :, 0], st)
-    np.testing.assert_allclose(lp2, ref, atol=1e-6)
+    ref_a, _ = gpu_step(s, chunk[:4, :, 0], st[:4])
+    ref_b, _ = gpu_step(s, chunk[4:, :, 0], st[4:])
+    np.testing.assert_allclose(lp2, np.concatenate([ref_a, ref_b]), atol=1e-6)
     with pytest.raises(ValueError):
         model.forward(chunk.astype(np.int64))
     model.session.close()
