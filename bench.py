@@ -25,6 +25,7 @@ import torch  # noqa: E402
 
 import tone_amd.config as C  # noqa: E402
 from tone_amd.model import ToneSession  # noqa: E402
+from tone_amd.shard import gather_logprobs  # noqa: E402
 from tone_amd.weights import synthetic_weights  # noqa: E402
 
 METRIC = "real-time-factor & streams/sec/node, 300 ms chunk, batch=1..4096"
@@ -125,14 +126,13 @@ def main() -> None:
     slabs = [torch.zeros((B, C.STATE_SIZE), dtype=torch.float16, device=dev) for _ in range(2)]
     signal = torch.empty((B, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32, device=dev)   # audio lands here
     logp = torch.empty((B, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * B, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev) if pg else None
     stream = torch.cuda.Stream(dev)
 
     def step(i: int) -> None:
         signal.copy_(pcm[i % args.chunks], non_blocking=True)
         sess.run(signal, slabs[i % 2], logp, slabs[(i + 1) % 2], stream=stream)
-        if pg is not None:
-            pg.all_gather_into_tensor(gathered, logp)
+        if pg is not None:   # host-decoding exchange: every rank's logprobs, in stream order
+            gather_logprobs(logp, world * B)
 
     torch.cuda.synchronize()
     with torch.cuda.stream(stream):

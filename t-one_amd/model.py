@@ -201,7 +201,10 @@ class StreamingCTCModel:
         state_dict (.pt, weights_only) or a directory holding one.  ``providers`` is accepted for
         signature compatibility; the MI355X device is chosen with ``device``."""
         del providers
-        return cls(ToneSession(load_weights(model_path), device=device, precision=precision, max_batch=max_batch))
+        p = Path(model_path)
+        if p.suffix == ".onnx":   # StreamingCTCPipeline.from_local passes dir/model.onnx (pipeline.py:213)
+            p = p.parent
+        return cls(ToneSession(load_weights(p), device=device, precision=precision, max_batch=max_batch))
 
     @classmethod
     def from_synthetic(cls, seed: int = 0, **kw) -> "StreamingCTCModel":
