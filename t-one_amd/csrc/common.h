@@ -31,6 +31,9 @@ constexpr int kSub1C = 32, kSub1Kt = 11, kSub1Kf = 21, kSub1F = 44, kSub1S = 10;
 constexpr int kSub2C = 64, kSub2Kt = 11, kSub2Kf = 11, kSub2F = 34, kSub2S = 8, kSub2Stride = 3;
 constexpr int kSub2In = kSub2S + kMelT;       // 38 time rows into conv2
 constexpr int kSubOut = kSub2C * kSub2F;      // 2176
+constexpr int kConv2K = kSub2Kt * kSub2Kf * kSub1C;   // 3872 = 121 taps x 32 channels
+constexpr int kConv2KPad = 3904;              // next multiple of 64 (bf16 K-step); pad tap has zero weights
+constexpr int kMelPowCols = 128;              // 81 power bins padded to 4 x 32
 
 // flat state offsets (elements, per stream)
 constexpr int64_t kOffPre = 0;
@@ -68,5 +71,20 @@ __device__ __forceinline__ float wave_max(float v) {
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float round_h(float x) { return __half2float(__float2half_rn(x)); }
+
+// Activation store: fp32, or bf16 bits when OBF (bf16 mode operands of the next GEMM).
+template <bool OBF>
+__device__ __forceinline__ void store_act(void* base, int64_t i, float v) {
+  if constexpr (OBF) {
+    __bf16 h = (__bf16)v;
+    static_cast<uint16_t*>(base)[i] = __builtin_bit_cast(uint16_t, h);
+  } else {
+    static_cast<float*>(base)[i] = v;
+  }
+}
+__device__ __forceinline__ void store_bf16(uint16_t* base, int64_t i, float v) {
+  __bf16 h = (__bf16)v;
+  base[i] = __builtin_bit_cast(uint16_t, h);
+}
 
 }  // namespace tone

@@ -9,7 +9,8 @@ constexpr float kInvSqrtD = 0.05103103630798288f;   // 384^-0.5 (submodules.py:5
 
 // ---------------------------------------------------------------------------------------------
 // RMSNorm (submodules.py:34-54) in place over rows of 384: one wave per row, 6 elements per lane.
-__global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, const float* __restrict__ w, int rows) {
+__global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, const float* __restrict__ w, int rows,
+                                                      uint16_t* __restrict__ shadow) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -24,11 +25,15 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, con
   ss = wave_sum(ss);
   const float den = sqrtf(ss) * kInvSqrtD + kRmsEps;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) xr[lane + 64 * i] = w[lane + 64 * i] * (v[i] / den);
+  for (int i = 0; i < 6; ++i) {
+    const float y = w[lane + 64 * i] * (v[i] / den);
+    xr[lane + 64 * i] = y;
+    if (shadow) store_bf16(shadow, (int64_t)row * kD + lane + 64 * i, y);
+  }
 }
 
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, hipStream_t st) {
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows);
+hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, hipStream_t st) {
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow);
   return hipGetLastError();
 }
 
@@ -37,9 +42,10 @@ hipError_t launch_rmsnorm(float* x, const float* w, int rows, hipStream_t st) {
 // to its last S rows (conformer_blocks.py:147-148); MultiHeadAttention.update_state attends over
 // kv = [cache_S ; xn] and keeps [cache_S[T:] ; xn] (submodules.py:295-302); update_after_layer
 // left-pads it with zeros to 30 rows (conformer_blocks.py:161-163).  xn = norm_self_att(r).
+template <bool OBF>
 __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restrict__ r, const float* __restrict__ norm_w,
                                                           StateRef s, int layer_slot, int T, int S,
-                                                          float* __restrict__ xn, float* __restrict__ kv) {
+                                                          void* __restrict__ xn, void* __restrict__ kv) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t cache = s.row(b) + kOffMhsa + (int64_t)layer_slot * kMhsaS * kD;
   const int TK = S + T;
@@ -55,8 +61,8 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
     for (int e = 0; e < 6; ++e) {
       const int c = lane + 64 * e;
       const float y = norm_w[c] * (v[e] / den);
-      xn[((int64_t)b * T + i) * kD + c] = y;
-      kv[((int64_t)b * TK + S + i) * kD + c] = y;
+      store_act<OBF>(xn, ((int64_t)b * T + i) * kD + c, y);
+      store_act<OBF>(kv, ((int64_t)b * TK + S + i) * kD + c, y);
       // new cache row (30 - S) + (S - T + i) = 30 - T + i holds xn[i]
       s.out[cache + (int64_t)(kMhsaS - T + i) * kD + c] = __float2half_rn(y);
     }
@@ -64,7 +70,7 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
   // cached rows: stored rows 30-S .. 29
   for (int i = tid; i < S * kD; i += 256) {
     const int j = i / kD, c = i % kD;
-    kv[((int64_t)b * TK + j) * kD + c] = __half2float(s.in[cache + (int64_t)(kMhsaS - S + j) * kD + c]);
+    store_act<OBF>(kv, ((int64_t)b * TK + j) * kD + c, __half2float(s.in[cache + (int64_t)(kMhsaS - S + j) * kD + c]));
   }
   // new cache rows 0 .. 30-T-1: zero padding below 30-S, then cache_S[T:]
   for (int i = tid; i < (kMhsaS - T) * kD; i += 256) {
@@ -75,9 +81,10 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
   }
 }
 
-hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S, float* xn,
-                              float* kv, int B, hipStream_t st) {
-  hipLaunchKernelGGL(kv_assemble_kernel, dim3(B), dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
+hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S, void* xn,
+                              void* kv, bool obf, int B, hipStream_t st) {
+  if (obf) hipLaunchKernelGGL(kv_assemble_kernel<true>, dim3(B), dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
+  else hipLaunchKernelGGL(kv_assemble_kernel<false>, dim3(B), dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
   return hipGetLastError();
 }
 
@@ -90,6 +97,7 @@ hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, i
 //              to layers 1-6 / 8-13, so softmax(shared scores) = shared probabilities)
 //   ctx = P . V
 constexpr int kMaxT = 10, kMaxTK = 40;
+template <bool OBF>
 __global__ void __launch_bounds__(64) attention_kernel(AttnArgs a) {
   __shared__ float qs[kMaxT][kDk + 1];
   __shared__ float ks[kMaxTK][kDk + 1];
@@ -174,13 +182,14 @@ __global__ void __launch_bounds__(64) attention_kernel(AttnArgs a) {
     const int i = e / kDk, d = e % kDk;
     float acc = 0.f;
     for (int j = 0; j < TK; ++j) acc = fmaf(ps[i][j], vs[j][d], acc);
-    a.ctx[((int64_t)b * T + i) * kD + h * kDk + d] = acc;
+    store_act<OBF>(a.ctx, ((int64_t)b * T + i) * kD + h * kDk + d, acc);
   }
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if (a.T > kMaxT || a.S + a.T > kMaxTK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attention_kernel, dim3(a.B * kHeads), dim3(64), 0, st, a);
+  if (a.ctx_bf16) hipLaunchKernelGGL(attention_kernel<true>, dim3(a.B * kHeads), dim3(64), 0, st, a);
+  else hipLaunchKernelGGL(attention_kernel<false>, dim3(a.B * kHeads), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -189,10 +198,10 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
 //   x = [conv state (30) ; g (T)] per channel; next state = x[-30:]
 //   out[t] = SiLU(BN(bias + sum_k w[k] x[t+k]))  with BN folded into (w, b) on the host.
 // One thread per (stream, channel).
-template <int T>
+template <int T, bool OBF>
 __global__ void __launch_bounds__(256) dwconv_kernel(const float* __restrict__ g, StateRef s, int layer,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
-                                                     float* __restrict__ out, int B) {
+                                                     void* __restrict__ out, int B) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= B * kD) return;
   const int b = idx / kD, c = idx % kD;
@@ -211,17 +220,19 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const float* __restrict__ g
     float acc = bb;
 #pragma unroll
     for (int k = 0; k < kConvK; ++k) acc = fmaf(wr[k], x[t + k], acc);
-    out[((int64_t)b * T + t) * kD + c] = silu_f(acc);
+    store_act<OBF>(out, ((int64_t)b * T + t) * kD + c, silu_f(acc));
   }
 #pragma unroll
   for (int i = 0; i < kConvS; ++i) s.out[st + i] = __float2half_rn(x[T + i]);
 }
 
-hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, float* out, int T,
-                         int B, hipStream_t st) {
+hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
+                         int T, int B, hipStream_t st) {
   const dim3 grid((B * kD + 255) / 256);
-  if (T == kT) hipLaunchKernelGGL(dwconv_kernel<kT>, grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
-  else if (T == kT / 2) hipLaunchKernelGGL(dwconv_kernel<kT / 2>, grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
+  if (T == kT && obf) hipLaunchKernelGGL((dwconv_kernel<kT, true>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
+  else if (T == kT) hipLaunchKernelGGL((dwconv_kernel<kT, false>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
+  else if (T == kT / 2 && obf) hipLaunchKernelGGL((dwconv_kernel<kT / 2, true>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
+  else if (T == kT / 2) hipLaunchKernelGGL((dwconv_kernel<kT / 2, false>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -230,9 +241,10 @@ hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, 
 // CausalTemporalReduction.forward streaming branch (conformer_blocks.py:888-907), grouped part:
 //   x = [state (1) ; x^T (10)] per channel; next state = x[:, -1:]
 //   y[o][t] = bias[o] + sum_{k<3} w[o][k] x[o/4][2t+k], o < 1536, t < 5
+template <bool OBF>
 __global__ void __launch_bounds__(256) reduce_conv_kernel(const float* __restrict__ x, StateRef s,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
-                                                          float* __restrict__ y, int B) {
+                                                          void* __restrict__ y, int B) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= B * kD) return;
   const int b = idx / kD, c = idx % kD;
@@ -245,30 +257,34 @@ __global__ void __launch_bounds__(256) reduce_conv_kernel(const float* __restric
     const int o = 4 * c + q;
     const float w0 = w[o * 3], w1 = w[o * 3 + 1], w2 = w[o * 3 + 2], bo = bias[o];
     for (int t = 0; t < kT / 2; ++t)
-      y[((int64_t)b * (kT / 2) + t) * (4 * kD) + o] = bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2];
+      store_act<OBF>(y, ((int64_t)b * (kT / 2) + t) * (4 * kD) + o, bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2]);
   }
 }
 
-hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, float* y, int B,
+hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
                               hipStream_t st) {
-  hipLaunchKernelGGL(reduce_conv_kernel, dim3((B * kD + 255) / 256), dim3(256), 0, st, x, s, w, b, y, B);
+  if (obf) hipLaunchKernelGGL(reduce_conv_kernel<true>, dim3((B * kD + 255) / 256), dim3(256), 0, st, x, s, w, b, y, B);
+  else hipLaunchKernelGGL(reduce_conv_kernel<false>, dim3((B * kD + 255) / 256), dim3(256), 0, st, x, s, w, b, y, B);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
 // TemporalUpsampling (conformer_blocks.py:955-988): repeat_interleave x2, trim to 10, + residual.
-__global__ void __launch_bounds__(256) upsample_add_kernel(float* __restrict__ x10, const float* __restrict__ x5, int B) {
+__global__ void __launch_bounds__(256) upsample_add_kernel(float* __restrict__ x10, const float* __restrict__ x5, int B,
+                                                           uint16_t* __restrict__ shadow) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)B * kT * kD) return;
   const int64_t row = idx / kD;
   const int c = idx % kD;
   const int64_t b = row / kT, t = row % kT;
-  x10[idx] = x5[(b * (kT / 2) + t / 2) * kD + c] + x10[idx];
+  const float v = x5[(b * (kT / 2) + t / 2) * kD + c] + x10[idx];
+  x10[idx] = v;
+  if (shadow) store_bf16(shadow, idx, v);
 }
 
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, hipStream_t st) {
+hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, hipStream_t st) {
   const int64_t n = (int64_t)B * kT * kD;
-  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B);
+  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, shadow);
   return hipGetLastError();
 }
 

@@ -2,65 +2,36 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace tone {
 
 // ---------------------------------------------------------------------------------------------
-// a1/a2.  Tone.forward_for_export raw branch (tone/nn/model.py:164-169) and
-// FilterbankFeatures.forward_streaming/_forward (tone/nn/modules/feats.py:95-102,118-133):
-//   wav = fp16(pcm / 32767); x = [state(80) ; wav] (2480); next state = x[-80:]
-//   spec[t][r] = sum_k basis[r][k] * x[80t + k]      (162 x 160 basis: DFT * Hann * pre-emphasis)
-//   power = re^2 + im^2 (81 bins); mel = fbank(64x81) . power; feats = fp16(log(mel + 2^-24))
-// One workgroup per stream; the 2480 samples and the 30x162 spectrum stay in LDS.
-// Also writes mhsa_len' = min(mhsa_len + 10, 30) (EncoderState.next, conformer_blocks.py:191).
-__global__ void __launch_bounds__(256) mel_kernel(const int32_t* __restrict__ pcm, StateRef s,
-                                                  const float* __restrict__ basis, const float* __restrict__ fbank,
-                                                  float* __restrict__ feats) {
-  __shared__ __attribute__((aligned(16))) float x[kWave];
-  __shared__ float spec[kMelT][kBasisRows + 1];
-  const int b = blockIdx.x, tid = threadIdx.x;
+// a1.  Tone.forward_for_export raw branch (tone/nn/model.py:164-165) and the streaming concat of
+// FilterbankFeatures.forward_streaming (tone/nn/modules/feats.py:128-133):
+//   wav = fp16(pcm / 32767); x = [state(80) ; wav] (2480 samples); next state = x[-80:]
+// x is stored as fp32 values for the spectrum GEMM (mel_gemms, gemm.hip).  Also writes
+// mhsa_len' = min(mhsa_len + 10, 30) (EncoderState.next, conformer_blocks.py:191).
+__global__ void __launch_bounds__(256) mel_prep_kernel(const int32_t* __restrict__ pcm, StateRef s,
+                                                       float* __restrict__ wave, int B) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)B * kWave) return;
+  const int b = (int)(idx / kWave), i = (int)(idx % kWave);
   const int64_t srow = s.row(b);
-  for (int i = tid; i < kWave; i += 256) {
-    __half hv;
-    if (i < kPreState) hv = s.in[srow + kOffPre + i];
-    else hv = __float2half_rn((float)pcm[(int64_t)b * kChunk + (i - kPreState)] / 32767.0f);
-    x[i] = __half2float(hv);
-    if (i >= kChunk) s.out[srow + kOffPre + (i - kChunk)] = hv;
-  }
-  if (tid == 0) {
+  __half hv;
+  if (i < kPreState) hv = s.in[srow + kOffPre + i];
+  else hv = __float2half_rn((float)pcm[(int64_t)b * kChunk + (i - kPreState)] / 32767.0f);
+  wave[idx] = __half2float(hv);
+  if (i >= kChunk) s.out[srow + kOffPre + (i - kChunk)] = hv;
+  if (i == 0) {
     const float ml = __half2float(s.in[srow + kOffMhsaLen]);
     s.out[srow + kOffMhsaLen] = __float2half_rn(fminf(ml + (float)kT, (float)kMhsaS));
   }
-  __syncthreads();
-  for (int p = tid; p < kMelT * kBasisRows; p += 256) {
-    const int t = p / kBasisRows, r = p % kBasisRows;
-    const float4* bw = reinterpret_cast<const float4*>(basis + r * kWin);
-    const float4* xw = reinterpret_cast<const float4*>(x + t * kHop);
-    float acc = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < kWin / 4; ++k) {
-      const float4 w = bw[k], v = xw[k];
-      acc = fmaf(w.x, v.x, acc);
-      acc = fmaf(w.y, v.y, acc);
-      acc = fmaf(w.z, v.z, acc);
-      acc = fmaf(w.w, v.w, acc);
-    }
-    spec[t][r] = acc;
-  }
-  __syncthreads();
-  for (int p = tid; p < kMelT * kMels; p += 256) {
-    const int t = p / kMels, m = p % kMels;
-    float acc = 0.f;
-    for (int f = 0; f < kBins; ++f) {
-      const float re = spec[t][f], im = spec[t][kBins + f];
-      acc = fmaf(fbank[m * kBins + f], re * re + im * im, acc);
-    }
-    feats[((int64_t)b * kMelT + t) * kMels + m] = round_h(logf(acc + 5.9604644775390625e-08f));
-  }
 }
 
-hipError_t launch_mel(const int32_t* pcm, StateRef s, const float* basis, const float* fbank, float* feats, int B,
-                      hipStream_t st) {
-  hipLaunchKernelGGL(mel_kernel, dim3(B), dim3(256), 0, st, pcm, s, basis, fbank, feats);
+hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, hipStream_t st) {
+  const int64_t n = (int64_t)B * kWave;
+  hipLaunchKernelGGL(mel_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pcm, s, wave, B);
   return hipGetLastError();
 }
 
@@ -77,10 +48,12 @@ constexpr int kK1 = kSub1Kt * kSub1Kf;      // 231
 constexpr int kK1P = 256;                   // padded K
 constexpr int kPos1 = kMelT * kSub1F;       // 1320
 
+template <bool OBF>   // x2 stored as bf16 bits (bf16 mode) or fp32
 __global__ void __launch_bounds__(256) sub1_kernel(const float* __restrict__ feats, StateRef s,
                                                    const float* __restrict__ pre_norm_w, const float* __restrict__ w1,
                                                    const float* __restrict__ scale1, const float* __restrict__ shift1,
-                                                   float* __restrict__ x2) {
+                                                   void* __restrict__ x2) {
+  using XT = typename std::conditional<OBF, __bf16, float>::type;
   __shared__ float x1[(kSub1S + kMelT) * kMels];
   __shared__ float wk[kSub1C][kK1P + 1];
   __shared__ int koff[kK1P];
@@ -104,10 +77,10 @@ __global__ void __launch_bounds__(256) sub1_kernel(const float* __restrict__ fea
     if (t >= kMelT - kSub1S) s.out[srow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
   }
   // carried conv2 input rows -> x2 rows 0..7 (channels-last)
-  float* xb = x2 + (int64_t)b * kSub2In * kSub1F * kSub1C;
+  XT* xb = static_cast<XT*>(x2) + (int64_t)b * kSub2In * kSub1F * kSub1C;
   for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 256) {
     const int c = i / (kSub2S * kSub1F), r = (i / kSub1F) % kSub2S, f = i % kSub1F;
-    xb[(r * kSub1F + f) * kSub1C + c] = __half2float(s.in[srow + kOffSub2 + i]);
+    xb[(r * kSub1F + f) * kSub1C + c] = (XT)__half2float(s.in[srow + kOffSub2 + i]);
   }
   __syncthreads();
   const int li = lane & 31, lh = lane >> 5;
@@ -129,7 +102,7 @@ __global__ void __launch_bounds__(256) sub1_kernel(const float* __restrict__ fea
       if (p >= kPos1) continue;
       const int t = p / kSub1F, f = p % kSub1F;
       const float y = silu_f(fmaf(acc[r], sc[c], sh[c]));
-      xb[((kSub2S + t) * kSub1F + f) * kSub1C + c] = y;
+      xb[((kSub2S + t) * kSub1F + f) * kSub1C + c] = (XT)y;
       if (t >= kMelT - kSub2S)
         s.out[srow + kOffSub2 + (c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
     }
@@ -137,8 +110,9 @@ __global__ void __launch_bounds__(256) sub1_kernel(const float* __restrict__ fea
 }
 
 hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const float* scale1,
-                       const float* shift1, float* x2, int B, hipStream_t st) {
-  hipLaunchKernelGGL(sub1_kernel, dim3(B), dim3(256), 0, st, feats, s, pre_norm_w, w1, scale1, shift1, x2);
+                       const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st) {
+  if (x2_bf16) hipLaunchKernelGGL(sub1_kernel<true>, dim3(B), dim3(256), 0, st, feats, s, pre_norm_w, w1, scale1, shift1, x2);
+  else hipLaunchKernelGGL(sub1_kernel<false>, dim3(B), dim3(256), 0, st, feats, s, pre_norm_w, w1, scale1, shift1, x2);
   return hipGetLastError();
 }
 

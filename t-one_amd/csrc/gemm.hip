@@ -4,17 +4,26 @@
 //
 // W is row-major [N][K] exactly like torch Linear / 1x1 Conv1d weights, so the B operand is read
 // K-contiguous like A.  Two arithmetic modes share one tiling:
-//   fp32: v_mfma_f32_32x32x2_f32  (exact fp32 products, fp32 accumulate; BASELINE config 2)
-//   bf16: v_mfma_f32_32x32x16_bf16 (A converted to bf16 while staging, fp32 accumulate; config 3)
+//   fp32: v_mfma_f32_32x32x2_f32   (exact fp32 products, fp32 accumulate; BASELINE config 2), BK = 32
+//   bf16: v_mfma_f32_32x32x16_bf16 (A rounded to bf16 while staging or already stored bf16, W bf16,
+//         fp32 accumulate; BASELINE config 3), BK = 64
+// A K-step always moves 128-byte rows of W into LDS.
+//
+// A rows are addressed as  row r -> (r / rpg) * gstride + (r % rpg) * lda  (rpg = 0: r * lda), which
+// covers plain activations and overlapping mel windows (hop 80 inside a 2480-sample stream), or are
+// gathered per (kt, kf) tap for the conv2 implicit GEMM.
 //
 // Fused epilogues (the reference ops they absorb):
 //   rowscale  RMSNorm folded into the GEMM: the gain is pre-multiplied into W's columns and the
-//             row's 1/(||a||/sqrt(K) + 1e-8) is computed from the staged A tile
+//             row's 1/(||a||/sqrt(K) + 1e-8) is computed from the staged fp32 A tile
 //             (submodules.py:34-54 feeding Linear/Conv1d with K = d_model = 384)
 //   STORE     + bias                                       (nn.Linear)
 //   RESID     R + alpha*(acc + bias)                       (residual adds, conformer_blocks.py:814-834)
 //   SWIGLU    silu(g + b1) * (v + bv) on interleaved 32-row W1/Wv blocks (conformer_blocks.py:479-482)
 //   GLU       (a + ba) * sigmoid(g + bg) on interleaved pw1 halves     (conformer_blocks.py:419-422)
+//   CONV2     SiLU(acc * bn_scale + bn_shift) scattered to the subsampling Linear's input
+//   POWER     re^2 + im^2 of interleaved 32-bin re/im blocks            (feats.py:98)
+//   LOGMEL    fp16(log(acc + 2^-24)) for the first 64 columns           (feats.py:99-102)
 //
 // Pipeline: A/W tiles of the next K-step are fetched into registers while the MFMAs run on the
 // current LDS buffer (two LDS buffers, one barrier per K-step).  When M*N gives too few tiles to
@@ -38,23 +47,113 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   __bf16 ha = (__bf16)a, hb = (__bf16)b;
   return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
 }
+__device__ __forceinline__ uint16_t bf16_bits(float a) {
+  __bf16 h = (__bf16)a;
+  return __builtin_bit_cast(uint16_t, h);
+}
 
-template <int BM, int BN, int WM, int WN, int EPI, bool BF16, bool SPLIT>
-__global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs p) {
+template <int BM_, int BN_, int WM_, int WN_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+};
+
+// Shared epilogue.  C/D map of v_mfma_*_32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+template <class TL, int EPI, bool CBF, bool SPLIT, int TM = TL::BM / TL::WM / 32, int TN = TL::BN / TL::WN / 32>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[TM][TN], const float* rden, int m0, int n0,
+                                              int wm, int wn, int lane) {
+  constexpr int WTM = TL::BM / TL::WM, WTN = TL::BN / TL::WN;
+  constexpr bool CONV2 = (EPI == EPI_CONV2);
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lrow = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int row = m0 + lrow;
+      if (row >= p.M) continue;
+      if constexpr (SPLIT) {
+        float* dst = p.ws + ((int64_t)blockIdx.y * p.M + row) * p.N;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 32 + lr] = acc[i][j][r];
+      } else if constexpr (CONV2) {
+        const int b = row / (kT * kSub2F), rem = row % (kT * kSub2F);
+        const int t = rem / kSub2F, f = rem % kSub2F;
+        const int64_t o = ((int64_t)b * kT + t) * kSubOut + f * kSub2C;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int c = n0 + wn * WTN + j * 32 + lr;
+          const float y = silu_f(fmaf(acc[i][j][r], p.scale[c], p.bias[c]));
+          if constexpr (CBF) static_cast<uint16_t*>(p.C)[o + c] = bf16_bits(y);
+          else static_cast<float*>(p.C)[o + c] = y;
+        }
+      } else if constexpr (EPI == EPI_LOGMEL) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WTN + j * 32 + lr;
+          if (col < p.n_out)
+            static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = round_h(logf(acc[i][j][r] + 5.9604644775390625e-08f));
+        }
+      } else if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+        const float den = p.rowscale ? rden[lrow] : 1.0f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WTN + j * 32 + lr;
+          float v = acc[i][j][r];
+          if (p.rowscale) v = v / den;
+          if (p.bias) v += p.bias[col];
+          if constexpr (EPI == EPI_RESID) v = p.R[(int64_t)row * p.ldr + col] + p.alpha * v;
+          if constexpr (CBF) static_cast<uint16_t*>(p.C)[(int64_t)row * p.ldc + col] = bf16_bits(v);
+          else static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = v;
+          if (p.C2) p.C2[(int64_t)row * p.ldc + col] = bf16_bits(v);   // bf16 shadow of the residual
+        }
+      } else {
+        const float den = p.rowscale ? rden[lrow] : 1.0f;
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp) {
+          const int cg = n0 + wn * WTN + 2 * jp * 32 + lr;   // packed column of the first member
+          float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
+          const int oc = (n0 + wn * WTN) / 2 + jp * 32 + lr;
+          float o;
+          if constexpr (EPI == EPI_POWER) {
+            o = g * g + u * u;
+          } else {
+            if (p.rowscale) { g = g / den; u = u / den; }
+            g += p.bias[cg];
+            u += p.bias[cg + 32];
+            if constexpr (EPI == EPI_SWIGLU) o = silu_f(g) * u;   // linear1 -> SiLU, times linearv
+            else o = g * sigmoid_f(u);                            // GLU: first half * sigmoid(second)
+          }
+          if constexpr (CBF) static_cast<uint16_t*>(p.C)[(int64_t)row * p.ldc + oc] = bf16_bits(o);
+          else static_cast<float*>(p.C)[(int64_t)row * p.ldc + oc] = o;
+        }
+      }
+    }
+  }
+}
+
+// MMA16: bf16 MFMA (W bf16); ABF: A stored bf16; CBF: C stored bf16 (STORE/SWIGLU/GLU/CONV2)
+template <class TL, int EPI, bool MMA16, bool ABF, bool CBF, bool SPLIT>
+__global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) {
+  constexpr int BM = TL::BM, BN = TL::BN, WM = TL::WM, WN = TL::WN;
   constexpr int NT = WM * WN * 64;
-  constexpr int BK = 32;
+  constexpr int BK = MMA16 ? 64 : 32;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
-  static_assert(EPI < EPI_SWIGLU || (TN % 2 == 0), "gated epilogues pair n-tiles");
-  static_assert(!SPLIT || EPI < EPI_SWIGLU, "split-K only for STORE/RESID");
+  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU || EPI == EPI_POWER);
   constexpr bool CONV2 = (EPI == EPI_CONV2);
-  constexpr int LDS_ROW = BF16 ? (BK + 8) : (BK + 4);  // elements; keeps ds_read_b128 conflict-free
-  using ST = typename std::conditional<BF16, uint16_t, float>::type;
-  constexpr int A_V = BM * BK / 4 / NT;                 // float4 of A per thread per k-tile
-  constexpr int W_VE = BF16 ? 8 : 4;                    // W elements per 16-byte vector
-  constexpr int W_V = BN * BK / W_VE / NT;              // 16-byte W vectors per thread
-  static_assert(A_V >= 1 && W_V >= 1, "tile too small for the thread count");
+  static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
+  static_assert(!PAIRED || (TN % 2 == 0), "paired epilogues pair n-tiles");
+  static_assert(!SPLIT || EPI == EPI_STORE || EPI == EPI_RESID, "split-K only for STORE/RESID");
+  static_assert(MMA16 || !ABF, "bf16 A needs the bf16 MFMA");
+  constexpr int LDS_ROW = BK + (MMA16 ? 8 : 4);          // elements; conflict-free ds_read_b128 rows
+  using ST = typename std::conditional<MMA16, uint16_t, float>::type;   // LDS / W element
+  using AT = typename std::conditional<ABF, uint16_t, float>::type;     // A element in memory
+  constexpr int AVE = 16 / sizeof(AT);                   // A elements per 16-byte vector
+  constexpr int A_V = BM * BK / AVE / NT;                // A vectors per thread per K-step
+  constexpr int WVE = 16 / sizeof(ST);
+  constexpr int W_V = BN * BK / WVE / NT;
+  constexpr int A_RV = BK / AVE;                         // vectors per A row per K-step
+  static_assert(A_V >= 1 && W_V >= 1 && (NT % A_RV) == 0, "tile too small for the thread count");
 
   __shared__ __attribute__((aligned(16))) ST As[2][BM * LDS_ROW];
   __shared__ __attribute__((aligned(16))) ST Bs[2][BN * LDS_ROW];
@@ -63,72 +162,87 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = p.N / BN;
-  const int bm = blockIdx.x / ntn, bn = blockIdx.x % ntn;
+  // XCD-aware order (blocks are dealt round-robin over the 8 XCDs): consecutive logical tiles,
+  // which share the same A rows, land on one XCD so the A tile is fetched into one L2 only.
+  int wgid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = wgid & 7, q = nwg >> 3, rr = nwg & 7;
+    wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
+  }
+  const int bm = wgid / ntn, bn = wgid % ntn;
   const int m0 = bm * BM, n0 = bn * BN;
   const int kb = SPLIT ? blockIdx.y * p.k_split : 0;
   const int nk = (SPLIT ? p.k_split : p.K) / BK;
-  const float* __restrict__ A = p.A;
+  const AT* __restrict__ A = static_cast<const AT*>(p.A);
 
-  f32x4 ra[A_V];
-  u32x4 rw[W_V];
-  float ss[A_V];
-  int64_t rowbase[CONV2 ? A_V : 1];
+  // per-thread A row offsets (rows are fixed for the whole K loop)
+  int64_t rowoff[A_V];
+  bool rvalid[A_V];
 #pragma unroll
-  for (int i = 0; i < A_V; ++i) ss[i] = 0.f;
-  if constexpr (CONV2) {
-    // output position (b, t, f) of A row r -> base of its receptive field in x2[b][38][44][32]
-#pragma unroll
-    for (int i = 0; i < A_V; ++i) {
-      const int r = (tid + i * NT) / (BK / 4);
-      const int pos = min(m0 + r, p.M - 1);
-      const int b = pos / (kT * kSub2F), rem = pos % (kT * kSub2F);
+  for (int i = 0; i < A_V; ++i) {
+    const int r = (tid + i * NT) / A_RV;
+    const int gm = min(m0 + r, p.M - 1);
+    rvalid[i] = (m0 + r) < p.M;
+    if constexpr (CONV2) {
+      const int b = gm / (kT * kSub2F), rem = gm % (kT * kSub2F);
       const int t = rem / kSub2F, f = rem % kSub2F;
-      rowbase[i] = (((int64_t)b * kSub2In + kSub2Stride * t) * kSub1F + f) * kSub1C;
+      rowoff[i] = (((int64_t)b * kSub2In + kSub2Stride * t) * kSub1F + f) * kSub1C;
+    } else {
+      rowoff[i] = p.rpg ? (int64_t)(gm / p.rpg) * p.gstride + (int64_t)(gm % p.rpg) * p.lda : (int64_t)gm * p.lda;
     }
   }
+
+  u32x4 ra[A_V];
+  u32x4 rw[W_V];
+  float ss[A_V];
+#pragma unroll
+  for (int i = 0; i < A_V; ++i) ss[i] = 0.f;
 
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A_V; ++i) {
-      const int idx = tid + i * NT, r = idx / (BK / 4), c = idx % (BK / 4);
-      const int gm = m0 + r;
-      const int gmc = gm < p.M ? gm : p.M - 1;        // clamped row; zeroed below (no branch)
+      const int c = (tid + i * NT) % A_RV;
       int64_t off;
       if constexpr (CONV2) {
-        const int tap = k0 / BK, kt = tap / kSub2Kf, kf = tap % kSub2Kf;
-        off = rowbase[i] + (kt * kSub1F + kf) * kSub1C + c * 4;
+        const int k = k0 + c * AVE, tap = k >> 5, ci = k & 31;
+        const int kt = tap / kSub2Kf, kf = tap % kSub2Kf;
+        off = tap < kSub2Kt * kSub2Kf ? rowoff[i] + (kt * kSub1F + kf) * kSub1C + ci : rowoff[i];
       } else {
-        off = (int64_t)gmc * p.lda + k0 + c * 4;
+        off = rowoff[i] + k0 + c * AVE;
       }
-      f32x4 v = *reinterpret_cast<const f32x4*>(A + off);
-      ra[i] = gm < p.M ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      const u32x4 v = *reinterpret_cast<const u32x4*>(A + off);
+      ra[i] = rvalid[i] ? v : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int i = 0; i < W_V; ++i) {
-      const int idx = tid + i * NT, r = idx / (BK / W_VE), c = idx % (BK / W_VE);
-      const ST* base = static_cast<const ST*>(p.W) + (int64_t)(n0 + r) * p.K + k0 + c * W_VE;
+      const int idx = tid + i * NT, r = idx / (BK / WVE), c = idx % (BK / WVE);
+      const ST* base = static_cast<const ST*>(p.W) + (int64_t)(n0 + r) * p.K + k0 + c * WVE;
       rw[i] = *reinterpret_cast<const u32x4*>(base);
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A_V; ++i) {
-      const int idx = tid + i * NT, r = idx / (BK / 4), c = idx % (BK / 4);
-      const f32x4 v = ra[i];
-      if (p.rowscale) ss[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-      if constexpr (BF16) {
-        u32x2 u;
-        u.x = pack_bf16x2(v.x, v.y);
-        u.y = pack_bf16x2(v.z, v.w);
-        *reinterpret_cast<u32x2*>(&As[buf][r * LDS_ROW + c * 4]) = u;
+      const int idx = tid + i * NT, r = idx / A_RV, c = idx % A_RV;
+      if constexpr (ABF) {
+        *reinterpret_cast<u32x4*>(&As[buf][r * LDS_ROW + c * AVE]) = ra[i];
       } else {
-        *reinterpret_cast<f32x4*>(&As[buf][r * LDS_ROW + c * 4]) = v;
+        const f32x4 v = __builtin_bit_cast(f32x4, ra[i]);
+        if (p.rowscale) ss[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        if constexpr (MMA16) {
+          u32x2 u;
+          u.x = pack_bf16x2(v.x, v.y);
+          u.y = pack_bf16x2(v.z, v.w);
+          *reinterpret_cast<u32x2*>(&As[buf][r * LDS_ROW + c * 4]) = u;
+        } else {
+          *reinterpret_cast<f32x4*>(&As[buf][r * LDS_ROW + c * 4]) = v;
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < W_V; ++i) {
-      const int idx = tid + i * NT, r = idx / (BK / W_VE), c = idx % (BK / W_VE);
-      *reinterpret_cast<u32x4*>(&Bs[buf][r * LDS_ROW + c * W_VE]) = rw[i];
+      const int idx = tid + i * NT, r = idx / (BK / WVE), c = idx % (BK / WVE);
+      *reinterpret_cast<u32x4*>(&Bs[buf][r * LDS_ROW + c * WVE]) = rw[i];
     }
   };
 
@@ -142,7 +256,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs p) {
 
   const int lr = lane & 31, lh = lane >> 5;
   auto compute = [&](int buf) {
-    if constexpr (BF16) {
+    if constexpr (MMA16) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         bf16x8 a[TM], b[TN];
@@ -191,145 +305,366 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(GemmArgs p) {
     compute(cur);
     if (kt + 1 >= nk) {
 #pragma unroll
-      for (int i = 0; i < A_V; ++i) ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};   // no double count in ss
+      for (int i = 0; i < A_V; ++i) ra[i] = u32x4{0u, 0u, 0u, 0u};   // no double count in ss
     }
     store(cur ^ 1);
     __syncthreads();
   }
 
-  if (p.rowscale) {
+  if constexpr (!ABF) {
+    if (p.rowscale) {
 #pragma unroll
-    for (int i = 0; i < A_V; ++i) {
-      float v = ss[i];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      const int idx = tid + i * NT, r = idx / (BK / 4);
-      if ((idx % (BK / 4)) == 0) {
-        if constexpr (SPLIT) {
-          if (bn == 0 && m0 + r < p.M) p.ws_ss[(int64_t)blockIdx.y * p.M + m0 + r] = v;
-        } else {
-          rden[r] = sqrtf(v) * p.inv_sqrt_k + kRmsEps;
+      for (int i = 0; i < A_V; ++i) {
+        float v = ss[i];
+#pragma unroll
+        for (int o = 1; o < A_RV; o <<= 1) v += __shfl_xor(v, o, 64);
+        const int idx = tid + i * NT, r = idx / A_RV;
+        if ((idx % A_RV) == 0) {
+          if constexpr (SPLIT) {
+            if (bn == 0 && m0 + r < p.M) p.ws_ss[(int64_t)blockIdx.y * p.M + m0 + r] = v;
+          } else {
+            rden[r] = sqrtf(v) * p.inv_sqrt_k + kRmsEps;
+          }
         }
       }
+      if constexpr (!SPLIT) __syncthreads();
     }
-    if constexpr (!SPLIT) __syncthreads();
   }
 
-  // ---- epilogue: C/D map of v_mfma_*_32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  gemm_epilogue<TL, EPI, CBF, SPLIT>(p, acc, rden, m0, n0, wm, wn, lane);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// bf16 GEMM with LDS-DMA staging.  Both operands are bf16 in memory; each K-step (64) moves
+// 128-byte rows of A and W straight into LDS with global_load_lds_dwordx4 (one wave instruction =
+// 8 rows x 128 B), the next K-step's DMA in flight while the MFMAs run on the current buffer.
+// LDS rows are lane-linear, so the ds_read_b128 bank spread comes from an XOR swizzle applied to
+// the per-lane SOURCE address (16-byte slot ^= row & 7) and undone on the read (guide rule 21).
+// A rowscale GEMM reads the bf16 shadow of the residual and takes each row's sum of squares from
+// its own A fragments (waves of the first N column only).
+// Split-K is a runtime mode here (p.k_split > 0: K slice blockIdx.y, raw partials to p.ws).
+template <class TL, int EPI, bool CBF>
+__global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArgs p) {
+  constexpr int BM = TL::BM, BN = TL::BN, WM = TL::WM, WN = TL::WN;
+  constexpr int kNWaves = WM * WN;
+  constexpr int BK = 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr bool CONV2 = (EPI == EPI_CONV2);
+  constexpr int A_I = BM / 8 / kNWaves, W_I = BN / 8 / kNWaves;     // DMA wave-instructions per K-step
+  static_assert(A_I >= 1 && W_I >= 1 && BM % (8 * kNWaves) == 0 && BN % (8 * kNWaves) == 0, "tile/wave mismatch");
+  constexpr int kStageElems = (BM + BN) * BK;                    // bf16 elements per buffer
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kStageElems + 2 * BM];   // one LDS object (+ rden)
+  float* rden = reinterpret_cast<float*>(lds + 2 * kStageElems);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = p.N / BN;
+  int wgid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = wgid & 7, q = nwg >> 3, rr = nwg & 7;
+    wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
+  }
+  const int bm = wgid / ntn, bn = wgid % ntn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const bool split = p.k_split > 0;
+  const int kb = split ? (int)blockIdx.y * p.k_split : 0;
+  const int nk = (split ? p.k_split : p.K) / BK;
+  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
+  const uint16_t* __restrict__ W = static_cast<const uint16_t*>(p.W);
+
+  const int lrow8 = lane >> 3, lslot = lane & 7;
+  int64_t aoff[A_I];
+  int aslot[A_I];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+  for (int i = 0; i < A_I; ++i) {
+    const int row = 8 * (wid + i * kNWaves) + lrow8;
+    const int gm = min(m0 + row, p.M - 1);
+    aslot[i] = lslot ^ (row & 7);
+    if constexpr (CONV2) {
+      const int b = gm / (kT * kSub2F), rem = gm % (kT * kSub2F);
+      const int t = rem / kSub2F, f = rem % kSub2F;
+      aoff[i] = (((int64_t)b * kSub2In + kSub2Stride * t) * kSub1F + f) * kSub1C;
+    } else {
+      aoff[i] = (p.rpg ? (int64_t)(gm / p.rpg) * p.gstride + (int64_t)(gm % p.rpg) * p.lda : (int64_t)gm * p.lda) +
+                aslot[i] * 8;
+    }
+  }
+  int64_t woff[W_I];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int lrow = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      const int row = m0 + lrow;
-      if (row >= p.M) continue;
-      if constexpr (SPLIT) {
-        float* dst = p.ws + ((int64_t)blockIdx.y * p.M + row) * p.N;
+  for (int i = 0; i < W_I; ++i) {
+    const int row = 8 * (wid + i * kNWaves) + lrow8;
+    woff[i] = (int64_t)(n0 + row) * p.K + (lslot ^ (row & 7)) * 8;
+  }
+
+  auto stage = [&](int buf, int k0) {
+    uint16_t* base = lds + buf * kStageElems;
+    (void)base;
+    (void)W;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 32 + lr] = acc[i][j][r];
-        continue;
-      } else if constexpr (CONV2) {
-        const int b = row / (kT * kSub2F), rem = row % (kT * kSub2F);
-        const int t = rem / kSub2F, f = rem % kSub2F;
-        float* dst = p.C + ((int64_t)b * kT + t) * kSubOut + f * kSub2C;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int c = n0 + wn * WTN + j * 32 + lr;
-          dst[c] = silu_f(fmaf(acc[i][j][r], p.scale[c], p.bias[c]));
-        }
-        continue;
+    for (int i = 0; i < A_I; ++i) {
+      const uint16_t* src;
+      if constexpr (CONV2) {
+        const int k = k0 + aslot[i] * 8, tap = k >> 5, ci = k & 31;
+        const int kt = tap / kSub2Kf, kf = tap % kSub2Kf;
+        src = A + (tap < kSub2Kt * kSub2Kf ? aoff[i] + (kt * kSub1F + kf) * kSub1C + ci : aoff[i]);
       } else {
-        const float den = p.rowscale ? rden[lrow] : 1.0f;
-        if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+        src = A + aoff[i] + k0;
+      }
+#if defined(__HIP_DEVICE_COMPILE__)   // amdgcn-only builtin; the host pass only sees the kernel's signature
+      __builtin_amdgcn_global_load_lds(src, base + (8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int col = n0 + wn * WTN + j * 32 + lr;
-            float v = acc[i][j][r];
-            if (p.rowscale) v = v / den;
-            if (p.bias) v += p.bias[col];
-            if constexpr (EPI == EPI_RESID) v = p.R[(int64_t)row * p.ldr + col] + p.alpha * v;
-            p.C[(int64_t)row * p.ldc + col] = v;
+    for (int i = 0; i < W_I; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(W + woff[i] + k0, base + (BM + 8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
+#endif
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float ss[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) ss[i] = 0.f;
+  const bool want_ss = p.rowscale && wn == 0;
+
+  const int lr = lane & 31, lh = lane >> 5;
+  auto compute = [&](int buf) {
+    const uint16_t* base = lds + buf * kStageElems;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int slot = ks * 2 + lh;
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 32 + lr;
+        a[i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((slot ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WTN + j * 32 + lr;
+        b[j] = *reinterpret_cast<const bf16x8*>(base + (BM + row) * BK + ((slot ^ (row & 7)) << 3));
+      }
+      if (want_ss) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = (float)a[i][e];
+            ss[i] = fmaf(v, v, ss[i]);
           }
-        } else {
+      }
 #pragma unroll
-          for (int jp = 0; jp < TN / 2; ++jp) {
-            const int cg = n0 + wn * WTN + 2 * jp * 32 + lr;   // packed column of the gate/first half
-            float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
-            if (p.rowscale) { g = g / den; u = u / den; }
-            g += p.bias[cg];
-            u += p.bias[cg + 32];
-            const int oc = (n0 + wn * WTN) / 2 + jp * 32 + lr;
-            float o;
-            if constexpr (EPI == EPI_SWIGLU) o = silu_f(g) * u;   // linear1 -> SiLU, times linearv
-            else o = g * sigmoid_f(u);                            // GLU: first half * sigmoid(second)
-            p.C[(int64_t)row * p.ldc + oc] = o;
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  stage(0, kb);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kb + (kt + 1) * BK);
+    compute(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (p.rowscale) {
+    if (want_ss) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float v = ss[i] + __shfl_xor(ss[i], 32, 64);
+        if (lh == 0) {
+          const int r = wm * WTM + i * 32 + lr;
+          if (split) {
+            if (bn == 0 && m0 + r < p.M) p.ws_ss[(int64_t)blockIdx.y * p.M + m0 + r] = v;
+          } else {
+            rden[r] = sqrtf(v) * p.inv_sqrt_k + kRmsEps;
           }
         }
       }
     }
+    __syncthreads();
   }
+  if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+    if (split) {
+      gemm_epilogue<TL, EPI_STORE, false, true>(p, acc, rden, m0, n0, wm, wn, lane);
+      return;
+    }
+  }
+  gemm_epilogue<TL, EPI, CBF, false>(p, acc, rden, m0, n0, wm, wn, lane);
 }
 
 // Split-K combine: fixed-order sum of the partials, then the STORE/RESID epilogue.
-template <int EPI>
+template <int EPI, bool CBF>
 __global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmArgs p, int nsplit) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;     // one float4 of C
   const int64_t n4 = (int64_t)p.M * (p.N / 4);
   if (idx >= n4) return;
   const int row = (int)(idx / (p.N / 4)), col = (int)(idx % (p.N / 4)) * 4;
-  float4 v = *reinterpret_cast<const float4*>(p.ws + (int64_t)row * p.N + col);
-  for (int s = 1; s < nsplit; ++s) {
-    const float4 w = *reinterpret_cast<const float4*>(p.ws + ((int64_t)s * p.M + row) * p.N + col);
-    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-  }
+  f32x4 v = *reinterpret_cast<const f32x4*>(p.ws + (int64_t)row * p.N + col);
+  for (int s = 1; s < nsplit; ++s) v += *reinterpret_cast<const f32x4*>(p.ws + ((int64_t)s * p.M + row) * p.N + col);
   if (p.rowscale) {
     float ss = 0.f;
     for (int s = 0; s < nsplit; ++s) ss += p.ws_ss[(int64_t)s * p.M + row];
     const float den = sqrtf(ss) * p.inv_sqrt_k + kRmsEps;
     v.x /= den; v.y /= den; v.z /= den; v.w /= den;
   }
-  if (p.bias) {
-    v.x += p.bias[col]; v.y += p.bias[col + 1]; v.z += p.bias[col + 2]; v.w += p.bias[col + 3];
-  }
-  float* dst = p.C + (int64_t)row * p.ldc + col;
+  if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + col);
   if constexpr (EPI == EPI_RESID) {
     const float* r = p.R + (int64_t)row * p.ldr + col;
     v.x = r[0] + p.alpha * v.x; v.y = r[1] + p.alpha * v.y; v.z = r[2] + p.alpha * v.z; v.w = r[3] + p.alpha * v.w;
   }
-  dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+  if constexpr (CBF) {
+    uint16_t* d = static_cast<uint16_t*>(p.C) + (int64_t)row * p.ldc + col;
+    d[0] = bf16_bits(v.x); d[1] = bf16_bits(v.y); d[2] = bf16_bits(v.z); d[3] = bf16_bits(v.w);
+  } else {
+    float* d = static_cast<float*>(p.C) + (int64_t)row * p.ldc + col;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  if (p.C2) {
+    uint16_t* d = p.C2 + (int64_t)row * p.ldc + col;
+    d[0] = bf16_bits(v.x); d[1] = bf16_bits(v.y); d[2] = bf16_bits(v.z); d[3] = bf16_bits(v.w);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool BF16>
-static hipError_t launch_cfg(const GemmArgs& a, int epi, int nsplit, hipStream_t st) {
-  const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
-  const dim3 block(WM * WN * 64);
-  if (nsplit > 1) {
-    GemmArgs b = a;
-    b.k_split = a.K / nsplit;
-    const dim3 grid(tiles, nsplit);
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, EPI_STORE, BF16, true>), grid, block, 0, st, b);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const int64_t n4 = (int64_t)a.M * (a.N / 4);
-    const dim3 g2((unsigned)((n4 + 255) / 256));
-    if (epi == EPI_RESID) hipLaunchKernelGGL(splitk_epilogue_kernel<EPI_RESID>, g2, dim3(256), 0, st, b, nsplit);
-    else hipLaunchKernelGGL(splitk_epilogue_kernel<EPI_STORE>, g2, dim3(256), 0, st, b, nsplit);
-    return hipGetLastError();
+template <class TL, int EPI, bool MMA16, bool ABF, bool CBF>
+static hipError_t launch_one(const GemmArgs& a, int nsplit, hipStream_t st) {
+  const int tiles = ((a.M + TL::BM - 1) / TL::BM) * (a.N / TL::BN);
+  const dim3 block(TL::WM * TL::WN * 64);
+  if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+    if (nsplit > 1) {
+      GemmArgs b = a;
+      b.k_split = a.K / nsplit;
+      hipLaunchKernelGGL((gemm_kernel<TL, EPI_STORE, MMA16, ABF, false, true>), dim3(tiles, nsplit), block, 0, st, b);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      const int64_t n4 = (int64_t)a.M * (a.N / 4);
+      hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, CBF>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, b,
+                         nsplit);
+      return hipGetLastError();
+    }
   }
-  const dim3 grid(tiles);
-  switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, EPI_STORE, BF16, false>), grid, block, 0, st, a); break;
-    case EPI_RESID: hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, EPI_RESID, BF16, false>), grid, block, 0, st, a); break;
-    case EPI_SWIGLU: hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, EPI_SWIGLU, BF16, false>), grid, block, 0, st, a); break;
-    case EPI_GLU: hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, EPI_GLU, BF16, false>), grid, block, 0, st, a); break;
-    default: return hipErrorInvalidValue;
-  }
+  hipLaunchKernelGGL((gemm_kernel<TL, EPI, MMA16, ABF, CBF, false>), dim3(tiles), block, 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t conv2_gemm(const float* x2, const void* w, const float* scale, const float* shift, float* flat, int B,
+template <class TL, bool MMA16, bool ABF, bool CBF>
+static hipError_t launch_epi(const GemmArgs& a, int epi, int nsplit, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return launch_one<TL, EPI_STORE, MMA16, ABF, CBF>(a, nsplit, st);
+    case EPI_RESID: return launch_one<TL, EPI_RESID, MMA16, ABF, false>(a, nsplit, st);
+    case EPI_SWIGLU: return launch_one<TL, EPI_SWIGLU, MMA16, ABF, CBF>(a, 1, st);
+    case EPI_GLU: return launch_one<TL, EPI_GLU, MMA16, ABF, CBF>(a, 1, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <class TL>
+static hipError_t launch_prec(const GemmArgs& a, int epi, bool bf16, int nsplit, hipStream_t st) {
+  if (!bf16) return launch_epi<TL, false, false, false>(a, epi, nsplit, st);
+  if (a.a_bf16)
+    return a.c_bf16 ? launch_epi<TL, true, true, true>(a, epi, nsplit, st) : launch_epi<TL, true, true, false>(a, epi, nsplit, st);
+  return a.c_bf16 ? launch_epi<TL, true, false, true>(a, epi, nsplit, st) : launch_epi<TL, true, false, false>(a, epi, nsplit, st);
+}
+
+template <class TL, int EPI, bool CBF>
+static hipError_t launch_glds(const GemmArgs& a, int nsplit, hipStream_t st) {
+  const int tiles = ((a.M + TL::BM - 1) / TL::BM) * (a.N / TL::BN);
+  const dim3 block(TL::WM * TL::WN * 64);
+  if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+    if (nsplit > 1) {
+      GemmArgs b = a;
+      b.k_split = a.K / nsplit;
+      hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI_STORE, false>), dim3(tiles, nsplit), block, 0, st, b);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      const int64_t n4 = (int64_t)a.M * (a.N / 4);
+      hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, CBF>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, b,
+                         nsplit);
+      return hipGetLastError();
+    }
+  }
+  GemmArgs c = a;
+  c.k_split = 0;
+  hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI, CBF>), dim3(tiles), block, 0, st, c);
+  return hipGetLastError();
+}
+
+template <class TL>
+static hipError_t launch_glds_epi(const GemmArgs& a, int epi, int nsplit, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return a.c_bf16 ? launch_glds<TL, EPI_STORE, true>(a, nsplit, st) : launch_glds<TL, EPI_STORE, false>(a, nsplit, st);
+    case EPI_RESID: return launch_glds<TL, EPI_RESID, false>(a, nsplit, st);
+    case EPI_SWIGLU: return a.c_bf16 ? launch_glds<TL, EPI_SWIGLU, true>(a, 1, st) : launch_glds<TL, EPI_SWIGLU, false>(a, 1, st);
+    case EPI_GLU: return a.c_bf16 ? launch_glds<TL, EPI_GLU, true>(a, 1, st) : launch_glds<TL, EPI_GLU, false>(a, 1, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// bf16 operands already in memory: LDS-DMA kernel
+static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
+  constexpr int kTarget = 512;
+  const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);
+  const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
+  if (t128 >= kTarget) return launch_glds_epi<Tile<128, 128, 2, 2>>(a, epi, 1, st);
+  int nsplit = 1;
+  if ((epi == EPI_STORE || epi == EPI_RESID) && a.ws && t64 < kTarget) {
+    const int ksteps = a.K / 64;
+    for (int s = 2; s <= 16; ++s) {
+      if (ksteps % s || ksteps / s < 3) continue;
+      if ((int64_t)s * a.M * a.N > a.ws_cap) break;
+      nsplit = s;
+      if (t64 * s >= kTarget) break;
+    }
+  }
+  if (nsplit > 1 || t64 >= kTarget / 2) return launch_glds_epi<Tile<64, 128, 2, 2>>(a, epi, nsplit, st);
+  return launch_glds_epi<Tile<32, 128, 1, 2>>(a, epi, 1, st);
+}
+
+hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
+  const int bk = bf16 ? 64 : 32;
+  if (bf16 && a.a_bf16) {
+    if (a.K % 64 != 0 || a.N % 128 != 0 || a.M <= 0 || (epi == EPI_RESID && a.c_bf16)) return hipErrorInvalidValue;
+    return gemm_bf16(a, epi, st);
+  }
+  if (a.K % bk != 0 || a.N % 128 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  if (!bf16 && (a.a_bf16 || a.c_bf16)) return hipErrorInvalidValue;
+  if (epi == EPI_RESID && a.c_bf16) return hipErrorInvalidValue;
+  constexpr int kTarget = 512;     // >= 2 tiles per CU on 256 CUs
+  const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);
+  const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
+  if (t128 >= kTarget) return launch_prec<Tile<128, 128, 2, 2>>(a, epi, bf16, 1, st);
+  int nsplit = 1;
+  if ((epi == EPI_STORE || epi == EPI_RESID) && a.ws && t64 < kTarget) {
+    // smallest split of the K-steps that reaches the target, keeping >= 3 K-steps per split
+    const int ksteps = a.K / bk;
+    for (int s = 2; s <= 16; ++s) {
+      if (ksteps % s || ksteps / s < 3) continue;
+      if ((int64_t)s * a.M * a.N > a.ws_cap) break;
+      nsplit = s;
+      if (t64 * s >= kTarget) break;
+    }
+  }
+  if (nsplit > 1 || t64 >= kTarget / 2) return launch_prec<Tile<64, 128, 2, 2>>(a, epi, bf16, nsplit, st);
+  return launch_prec<Tile<32, 128, 1, 2>>(a, epi, bf16, 1, st);
+}
+
+hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
                       bool bf16, hipStream_t st) {
   GemmArgs a{};
   a.A = x2;
@@ -339,33 +674,47 @@ hipError_t conv2_gemm(const float* x2, const void* w, const float* scale, const 
   a.scale = scale;
   a.M = B * kT * kSub2F;
   a.N = kSub2C;
-  a.K = kSub2Kt * kSub2Kf * kSub1C;
+  a.K = bf16 ? kConv2KPad : kSub2Kt * kSub2Kf * kSub1C;
   const dim3 grid((a.M + 127) / 128), block(256);
-  if (bf16) hipLaunchKernelGGL((gemm_kernel<128, 64, 4, 1, EPI_CONV2, true, false>), grid, block, 0, st, a);
-  else hipLaunchKernelGGL((gemm_kernel<128, 64, 4, 1, EPI_CONV2, false, false>), grid, block, 0, st, a);
+  if (bf16) hipLaunchKernelGGL((gemm_glds_kernel<Tile<128, 64, 4, 1>, EPI_CONV2, true>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((gemm_kernel<Tile<128, 64, 4, 1>, EPI_CONV2, false, false, false, false>), grid, block, 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
-  if (a.K % 32 != 0 || a.N % 128 != 0 || a.M <= 0) return hipErrorInvalidValue;
-  constexpr int kTarget = 512;     // >= 2 tiles per CU on 256 CUs
-  const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);
-  const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
-  if (t128 >= kTarget) return bf16 ? launch_cfg<128, 128, 2, 2, true>(a, epi, 1, st) : launch_cfg<128, 128, 2, 2, false>(a, epi, 1, st);
-  int nsplit = 1;
-  if ((epi == EPI_STORE || epi == EPI_RESID) && a.ws && t64 < kTarget) {
-    // smallest split of the K-steps that reaches the target, keeping >= 3 K-steps per split
-    const int ksteps = a.K / 32;
-    for (int s = 2; s <= 16; ++s) {
-      if (ksteps % s || ksteps / s < 3) continue;
-      if ((int64_t)s * a.M * a.N > a.ws_cap) break;
-      nsplit = s;
-      if (t64 * s >= kTarget) break;
-    }
-  }
-  if (nsplit > 1 || t64 >= kTarget / 2)
-    return bf16 ? launch_cfg<64, 128, 2, 2, true>(a, epi, nsplit, st) : launch_cfg<64, 128, 2, 2, false>(a, epi, nsplit, st);
-  return bf16 ? launch_cfg<32, 128, 1, 2, true>(a, epi, 1, st) : launch_cfg<32, 128, 1, 2, false>(a, epi, 1, st);
+// Log-mel as two fp32-MFMA GEMMs over all B*30 frames (feats.py:95-102):
+//   power[(b,t)][f] = |sum_k basis_f[k] wave[b][80t + k]|^2      K = 160, N = 256 (re/im blocks)
+//   feats[(b,t)][m] = fp16(log(sum_f fbank[m][f] power[f] + 2^-24))  K = 128, N = 128 (64 used)
+hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank_p, float* power, float* feats, int B,
+                     hipStream_t st) {
+  GemmArgs a{};
+  a.A = wave;
+  a.lda = kHop;
+  a.rpg = kMelT;
+  a.gstride = kWave;
+  a.W = basis_p;
+  a.C = power;
+  a.ldc = kMelPowCols;
+  a.M = B * kMelT;
+  a.N = 2 * kMelPowCols;
+  a.K = kWin;
+  const dim3 block(256);
+  hipLaunchKernelGGL((gemm_kernel<Tile<64, 128, 2, 2>, EPI_POWER, false, false, false, false>),
+                     dim3(((a.M + 63) / 64) * (a.N / 128)), block, 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  GemmArgs m{};
+  m.A = power;
+  m.lda = kMelPowCols;
+  m.W = fbank_p;
+  m.C = feats;
+  m.ldc = kMels;
+  m.n_out = kMels;
+  m.M = B * kMelT;
+  m.N = 128;
+  m.K = kMelPowCols;
+  hipLaunchKernelGGL((gemm_kernel<Tile<64, 128, 2, 2>, EPI_LOGMEL, false, false, false, false>),
+                     dim3((m.M + 63) / 64), block, 0, st, m);
+  return hipGetLastError();
 }
 
 }  // namespace tone

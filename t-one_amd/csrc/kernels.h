@@ -9,13 +9,13 @@
 
 namespace tone {
 
-enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GLU = 3, EPI_CONV2 = 4 };
+enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GLU = 3, EPI_CONV2 = 4, EPI_POWER = 5, EPI_LOGMEL = 6 };
 
 struct GemmArgs {
-  const float* A;
+  const void* A;      // [M][K] fp32, or bf16 bits when a_bf16
   int64_t lda;
   const void* W;      // [N][K], fp32 or bf16 (raw bits)
-  float* C;
+  void* C;            // fp32, or bf16 bits when c_bf16
   int64_t ldc;
   const float* bias;  // packed like W's rows, or nullptr
   const float* R;     // residual (EPI_RESID); may alias C
@@ -30,6 +30,11 @@ struct GemmArgs {
   int64_t ws_cap;     // floats available in ws
   int k_split;        // set by the launcher
   const float* scale; // EPI_CONV2: folded BatchNorm scale per output channel (bias = shift)
+  int a_bf16, c_bf16; // bf16 mode only: A stored bf16 / C stored bf16
+  int rpg;            // A row grouping: row r at (r / rpg) * gstride + (r % rpg) * lda (0 = off)
+  int64_t gstride;
+  int n_out;          // EPI_LOGMEL: columns written
+  uint16_t* C2;       // STORE/RESID: optional bf16 shadow of C (same ldc), feeds bf16 GEMMs
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -37,31 +42,35 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
 // a3 conv2 as an implicit GEMM over all streams: A rows gathered from the channels-last
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,
 // epilogue SiLU(acc*scale + shift) -> flat [B*10][34*64] (f-major, channel-minor).
-hipError_t conv2_gemm(const float* x2, const void* w, const float* scale, const float* shift, float* flat, int B,
+hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
                       bool bf16, hipStream_t st);
 
-// a1/a2: PCM -> fp16 -> log-mel fp16 features [B][30][64] (stored as fp32 values); preproc state
+// a2 log-mel on the fp32 MFMA: power spectrum GEMM over overlapping windows, then filterbank GEMM
+// with the log / fp16 epilogue.  wave [B][2480] fp32 (from launch_mel_prep).
+hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank_p, float* power, float* feats, int B,
+                     hipStream_t st);
+
+// a1: PCM -> fp16 wave [B][2480] (fp32 storage) with the 80 carried samples; next preproc state
 // and mhsa_len of the next state.
-hipError_t launch_mel(const int32_t* pcm, StateRef s, const float* basis, const float* fbank, float* feats, int B,
-                      hipStream_t st);
+hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, hipStream_t st);
 
 // a3 part 1: pre-norm RMSNorm(64) + sub1 state + Conv2d(1->32,k11x21) + BN + SiLU, written with the
 // carried sub2 rows as the channels-last conv2 input x2 [B][38][44][32]; next sub1/sub2 states.
 hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const float* scale1,
-                       const float* shift1, float* x2, int B, hipStream_t st);
+                       const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st);
 
-// In-place RMSNorm over rows of 384 (norm_out, out_norm).
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, hipStream_t st);
+// In-place RMSNorm over rows of 384 (norm_out, out_norm); optional bf16 shadow of the result.
+hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, hipStream_t st);
 
 // Layers 14/15: xn = RMSNorm(r); kv = [cache(S rows) ; xn]; next cache (left-padded to 30) -> state.
 hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S,
-                              float* xn, float* kv, int B, hipStream_t st);
+                              void* xn, void* kv, bool obf, int B, hipStream_t st);
 
 struct AttnArgs {
   const float* q; int64_t ldq;      // rows b*T+i
   const float* k; int64_t ldk;      // rows b*(S+T)+j
   const float* v; int64_t ldv;      // rows b*(S+T)+j
-  float* ctx;                       // [B*T][384]
+  void* ctx;                        // [B*T][384], fp32 or bf16 (ctx_bf16)
   float* probs;                     // [B][8][T][S+T]: written when scores are computed, read when shared
   const float* qln_w; const float* qln_b; const float* kln_w; const float* kln_b;
   const float* rope_cos;            // [40][16] positions -30..9 (row = pos + 30)
@@ -71,19 +80,20 @@ struct AttnArgs {
   int recompute;                    // 1: q,k -> LN -> RoPE -> scores; 0: reuse probs
   int reduced;                      // mask offset floor-divided by 2 (layer 14)
   int B;
+  int ctx_bf16;
 };
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 
 // a9: depthwise causal conv k31 with carried state + folded BatchNorm + SiLU.
-hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, float* out, int T,
-                         int B, hipStream_t st);
+hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
+                         int T, int B, hipStream_t st);
 
 // a11: reduction state + grouped conv (384->1536, k3, s2) -> y [B*5][1536]
-hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, float* y, int B,
+hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
                               hipStream_t st);
 
 // a12: x10[b*10+t] += x5[b*5+t/2]
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, hipStream_t st);
+hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, hipStream_t st);
 
 // a14: logits = x . Wd^T + bd, log_softmax over 35 classes -> logprobs [B*10][35]
 hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int rows, hipStream_t st);

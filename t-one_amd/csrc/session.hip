@@ -79,7 +79,7 @@ struct tone_session {
   int64_t dev_bytes = 0;
 
   // weights
-  float *basis, *fbank, *rope_cos, *rope_sin;
+  float *basis_p, *fbank_p, *rope_cos, *rope_sin;
   float *pre_norm, *w1, *scale1, *shift1, *scale2, *shift2, *out_norm;
   void* w2c;
   void* wsub_out;
@@ -89,7 +89,9 @@ struct tone_session {
   LayerW L[16];
 
   // activations
-  float *feats, *x2, *flat, *rA, *rB, *h, *qkv, *xn, *kv, *kvp, *ctx, *g, *d, *probs, *yred;
+  float *wave, *power, *feats, *rA, *rB, *qkv, *kvp, *g, *probs;
+  void *x2, *flat, *h, *ctx, *d, *xn, *kv, *yred;   // bf16 in bf16 mode
+  uint16_t *xbA, *xbB;                              // bf16 shadows of rA / rB (bf16 mode)
   float *ws, *ws_ss;
   int64_t ws_cap = 0;
 
@@ -273,10 +275,10 @@ struct Scope {
     if (_e != hipSuccess) return fail(TONE_E_HIP, std::string(fam) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-int gemm_call(tone_session* s, hipStream_t st, const char* fam, const float* A, int64_t lda, const void* W, float* C,
+int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, int64_t lda, const void* W, void* C,
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
-              float alpha = 1.0f) {
-  GemmArgs a;
+              float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr) {
+  GemmArgs a{};   // value-initialised: every field not set below is zero
   a.A = A;
   a.lda = lda;
   a.W = W;
@@ -295,6 +297,10 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const float* A, 
   a.ws_ss = s->ws_ss;
   a.ws_cap = s->ws_cap;
   a.k_split = 0;
+  const bool bf = s->precision == TONE_PRECISION_BF16;
+  a.a_bf16 = bf && a_bf16;
+  a.c_bf16 = bf && c_bf16;
+  a.C2 = bf ? c2 : nullptr;
   LAUNCH(fam, gemm(a, epi, s->precision == TONE_PRECISION_BF16, st));
   return TONE_OK;
 }
@@ -306,27 +312,38 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const float* A, 
   } while (0)
 
 // The whole streaming step (Tone.forward_for_export, model.py:162-205).
+// bf16 mode: every GEMM operand is bf16 in memory -- the residual keeps an fp32 master copy plus a
+// bf16 shadow written by each of its producers; the other operands are produced in bf16 directly.
 int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* logp, int B, hipStream_t st) {
   const int D = kD;
-  LAUNCH("mel", launch_mel(signal, sr, s->basis, s->fbank, s->feats, B, st));
+  const bool bf = s->precision == TONE_PRECISION_BF16;
+  uint16_t* shA = bf ? s->xbA : nullptr;
+  uint16_t* shB = bf ? s->xbB : nullptr;
+  LAUNCH("mel_prep", launch_mel_prep(signal, sr, s->wave, B, st));
+  LAUNCH("mel", mel_gemms(s->wave, s->basis_p, s->fbank_p, s->power, s->feats, B, st));
   if (s->debug_stop == 0) return TONE_OK;
-  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->scale1, s->shift1, s->x2, B, st));
-  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, s->precision == TONE_PRECISION_BF16, st));
+  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->scale1, s->shift1, s->x2, bf, B, st));
+  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * kT, D, kSubOut,
-                 EPI_STORE, 0));
-  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, st));
+                 EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
+  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, shA, st));
   if (s->debug_stop == 1) return TONE_OK;
   float* x = s->rA;
+  uint16_t* xs = shA;           // bf16 shadow of x (bf16 mode)
   int T = kT;
   for (int l = 0; l < 16; ++l) {
     const LayerW& w = s->L[l];
     const int M = B * T;
-    // FFN1 (conformer_blocks.py:812-814)
-    CALL(gemm_call(s, st, "gemm_ffn_up", x, D, w.w13[0], s->h, kDff, w.b13[0], M, 2 * kDff, D, EPI_SWIGLU, 1));
-    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[0], x, D, w.b2[0], M, D, kDff, EPI_RESID, 0, x, 0.5f));
+    const void* xa = bf ? static_cast<const void*>(xs) : x;   // A operand of the rowscale GEMMs
+    // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
+    CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[0], s->h, kDff, w.b13[0], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
+                   1.0f, true, true));
+    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[0], x, D, w.b2[0], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
+                   false, xs));
     // MHSA (conformer_blocks.py:816-825)
     AttnArgs aa{};
     aa.ctx = s->ctx;
+    aa.ctx_bf16 = bf;
     aa.probs = s->probs;
     aa.qln_w = w.qln_w;
     aa.qln_b = w.qln_b;
@@ -340,7 +357,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     if (l < 14) {
       const bool rec = (l == 0 || l == 7);
       const int N = rec ? 3 * D : D;
-      CALL(gemm_call(s, st, "gemm_qkv", x, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1));
+      CALL(gemm_call(s, st, "gemm_qkv", xa, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1, nullptr, 1.0f, true));
       aa.S = 0;
       aa.recompute = rec;
       aa.reduced = 0;
@@ -353,9 +370,10 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       }
     } else {
       const int S = (l == 14) ? kMhsaS / 2 : kMhsaS;
-      LAUNCH("kv_assemble", launch_kv_assemble(x, w.norm_att, sr, l - 14, T, S, s->xn, s->kv, B, st));
-      CALL(gemm_call(s, st, "gemm_qkv", s->xn, D, w.wq, s->qkv, D, w.bq, M, D, D, EPI_STORE, 0));
-      CALL(gemm_call(s, st, "gemm_qkv", s->kv, D, w.wkv, s->kvp, 2 * D, w.bkv, B * (S + T), 2 * D, D, EPI_STORE, 0));
+      LAUNCH("kv_assemble", launch_kv_assemble(x, w.norm_att, sr, l - 14, T, S, s->xn, s->kv, bf, B, st));
+      CALL(gemm_call(s, st, "gemm_qkv", s->xn, D, w.wq, s->qkv, D, w.bq, M, D, D, EPI_STORE, 0, nullptr, 1.0f, true));
+      CALL(gemm_call(s, st, "gemm_qkv", s->kv, D, w.wkv, s->kvp, 2 * D, w.bkv, B * (S + T), 2 * D, D, EPI_STORE, 0,
+                     nullptr, 1.0f, true));
       aa.S = S;
       aa.recompute = 1;
       aa.reduced = (l == 14);
@@ -365,25 +383,29 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       aa.v = s->kvp + D; aa.ldv = 2 * D;
     }
     LAUNCH("attention", launch_attention(aa, st));
-    CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f));
+    CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
     // Convolution module (conformer_blocks.py:827-830)
-    CALL(gemm_call(s, st, "gemm_pw1", x, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1));
-    LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, T, B, st));
-    CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f));
+    CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true));
+    LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st));
+    CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
     // FFN2 + norm_out (conformer_blocks.py:832-836)
-    CALL(gemm_call(s, st, "gemm_ffn_up", x, D, w.w13[1], s->h, kDff, w.b13[1], M, 2 * kDff, D, EPI_SWIGLU, 1));
-    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[1], x, D, w.b2[1], M, D, kDff, EPI_RESID, 0, x, 0.5f));
-    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, st));
+    CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[1], s->h, kDff, w.b13[1], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
+                   1.0f, true, true));
+    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[1], x, D, w.b2[1], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
+                   false, xs));
+    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, st));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
-      LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, B, st));
+      LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, st));
       CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * (kT / 2), D, 4 * D,
-                     EPI_STORE, 0));
+                     EPI_STORE, 0, nullptr, 1.0f, true, false, shB));
       x = s->rB;
+      xs = shB;
       T = kT / 2;
     }
     if (l == 14) {  // TemporalUpsampling (conformer.py:224-225)
-      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, st));
+      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, shA, st));
       x = s->rA;
+      xs = shA;
       T = kT;
     }
     if (s->debug_stop == 2 + l) return TONE_OK;
@@ -420,8 +442,25 @@ int finalize_weights(tone_session* s) {
   auto hb = W("decoder.decoder_layers.0.bias", 35);
   if (!miss.empty()) return fail(TONE_E_MISSING, "missing or mis-sized weight: " + miss);
 
-  CALL(upload(s, &s->basis, make_basis()));
-  CALL(upload(s, &s->fbank, make_fbank()));
+  {  // spectrum GEMM weight [256][160]: 32-bin blocks of Re rows then Im rows (bins >= 81 zero)
+    const std::vector<float> basis = make_basis();   // [162][160]: rows 0..80 Re, 81..161 Im
+    std::vector<float> bp((size_t)2 * kMelPowCols * kWin, 0.f);
+    for (int q = 0; q < kMelPowCols / 32; ++q)
+      for (int r = 0; r < 32; ++r) {
+        const int f = 32 * q + r;
+        if (f >= kBins) continue;
+        for (int k = 0; k < kWin; ++k) {
+          bp[(size_t)(64 * q + r) * kWin + k] = basis[(size_t)f * kWin + k];
+          bp[(size_t)(64 * q + 32 + r) * kWin + k] = basis[(size_t)(kBins + f) * kWin + k];
+        }
+      }
+    CALL(upload(s, &s->basis_p, bp));
+    const std::vector<float> fb = make_fbank();      // [64][81]
+    std::vector<float> fp((size_t)128 * kMelPowCols, 0.f);
+    for (int m = 0; m < kMels; ++m)
+      for (int f = 0; f < kBins; ++f) fp[(size_t)m * kMelPowCols + f] = fb[(size_t)m * kBins + f];
+    CALL(upload(s, &s->fbank_p, fp));
+  }
   std::vector<float> cs, sn;
   make_rope(cs, sn);
   CALL(upload(s, &s->rope_cos, cs));
@@ -447,10 +486,11 @@ int finalize_weights(tone_session* s) {
       sh[c] = (float)(((double)(*c2b)[c] - (double)(*bn2[2])[c]) * scale + (double)(*bn2[1])[c]);
     }
     // conv2 weight tap-major [c2][kt][kf][ci] for the implicit GEMM over channels-last input
-    std::vector<float> w2r((size_t)64 * 121 * 32);
+    const int kw = s->precision == TONE_PRECISION_BF16 ? kConv2KPad : kConv2K;   // bf16: zero pad tap
+    std::vector<float> w2r((size_t)64 * kw, 0.f);
     for (int c2 = 0; c2 < 64; ++c2)
       for (int ci = 0; ci < 32; ++ci)
-        for (int k = 0; k < 121; ++k) w2r[((size_t)c2 * 121 + k) * 32 + ci] = (*c2w)[((size_t)c2 * 32 + ci) * 121 + k];
+        for (int k = 0; k < 121; ++k) w2r[(size_t)c2 * kw + k * 32 + ci] = (*c2w)[((size_t)c2 * 32 + ci) * 121 + k];
     CALL(upload_w(s, &s->w2c, w2r));
     CALL(upload(s, &s->scale2, sc));
     CALL(upload(s, &s->shift2, sh));
@@ -590,21 +630,25 @@ int finalize_weights(tone_session* s) {
 
   // activations
   const size_t MB = (size_t)s->max_batch;
+  CALL(dalloc(s, &s->wave, MB * kWave));
+  CALL(dalloc(s, &s->power, MB * kMelT * kMelPowCols));
   CALL(dalloc(s, &s->feats, MB * kMelT * kMels));
-  CALL(dalloc(s, &s->x2, MB * kSub2In * kSub1F * kSub1C));
-  CALL(dalloc(s, &s->flat, MB * kT * kSubOut));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->x2), MB * kSub2In * kSub1F * kSub1C));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->flat), MB * kT * kSubOut));
   CALL(dalloc(s, &s->rA, MB * kT * D));
   CALL(dalloc(s, &s->rB, MB * (kT / 2) * D));
-  CALL(dalloc(s, &s->h, MB * kT * kDff));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->h), MB * kT * kDff));
   CALL(dalloc(s, &s->qkv, MB * kT * 3 * D));
-  CALL(dalloc(s, &s->xn, MB * kT * D));
-  CALL(dalloc(s, &s->kv, MB * 40 * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->xn), MB * kT * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->kv), MB * 40 * D));
   CALL(dalloc(s, &s->kvp, MB * 40 * 2 * D));
-  CALL(dalloc(s, &s->ctx, MB * kT * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->ctx), MB * kT * D));
   CALL(dalloc(s, &s->g, MB * kT * D));
-  CALL(dalloc(s, &s->d, MB * kT * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->d), MB * kT * D));
   CALL(dalloc(s, &s->probs, MB * kHeads * kT * 40));
-  CALL(dalloc(s, &s->yred, MB * (kT / 2) * 4 * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->yred), MB * (kT / 2) * 4 * D));
+  CALL(dalloc(s, &s->xbA, MB * kT * D));
+  CALL(dalloc(s, &s->xbB, MB * (kT / 2) * D));
   // split-K workspace: only small batches split (large ones fill the chip with whole-K tiles)
   s->ws_cap = 16ll << 20;
   CALL(dalloc(s, &s->ws, (size_t)s->ws_cap));
@@ -749,8 +793,8 @@ int tone_session_debug_read(tone_session* s, const char* buffer, void* host_dst,
   const float* p = nullptr;
   size_t cap = 0;
   if (n == "feats") { p = s->feats; cap = MB * kMelT * kMels; }
-  else if (n == "x2") { p = s->x2; cap = MB * kSub2In * kSub1F * kSub1C; }
-  else if (n == "flat") { p = s->flat; cap = MB * kT * kSubOut; }
+  else if (n == "x2") { p = static_cast<const float*>(s->x2); cap = MB * kSub2In * kSub1F * kSub1C; }
+  else if (n == "flat") { p = static_cast<const float*>(s->flat); cap = MB * kT * kSubOut; }
   else if (n == "rA") { p = s->rA; cap = MB * kT * kD; }
   else if (n == "rB") { p = s->rB; cap = MB * (kT / 2) * kD; }
   else return fail(TONE_E_INVALID, "unknown debug buffer " + n);
