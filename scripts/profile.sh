@@ -10,9 +10,9 @@ run() {  # name, limit, command...
   echo "$name rc=$rc"
   if [ $rc -gt 1 ]; then exit $rc; fi
 }
-run "bench_$tag" 300 python bench.py --cpu-baseline-s 0 "$@"
-run "stats_$tag" 400 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$tag" -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-baseline-s 0 "$@"
+run "bench_$tag" 300 python bench.py --cpu-baseline-s 0 --alt 0 "$@"
+run "stats_$tag" 400 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$tag" -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --cpu-baseline-s 0 --alt 0 "$@"
 if [ "${PMC:-0}" = 1 ]; then
-  run "pmcf_$tag" 400 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/pmcf_$tag" -o run --output-format csv -- python bench.py --steps 2 --warmup 2 --no-graph --cpu-baseline-s 0 "$@"
-  run "pmcw_$tag" 400 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/pmcw_$tag" -o run --output-format csv -- python bench.py --steps 2 --warmup 2 --no-graph --cpu-baseline-s 0 "$@"
+  run "pmcf_$tag" 400 rocprofv3 --pmc FETCH_SIZE -d "gpurun_out/pmcf_$tag" -o run --output-format csv -- python bench.py --steps 2 --warmup 2 --no-graph --cpu-baseline-s 0 --alt 0 "$@"
+  run "pmcw_$tag" 400 rocprofv3 --pmc WRITE_SIZE -d "gpurun_out/pmcw_$tag" -o run --output-format csv -- python bench.py --steps 2 --warmup 2 --no-graph --cpu-baseline-s 0 --alt 0 "$@"
 fi

@@ -90,56 +90,76 @@ hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, i
 
 // ---------------------------------------------------------------------------------------------
 // RotaryMultiHeadAttention.forward (conformer_blocks.py:688-726) + forward_qkv/forward_attention
-// (submodules.py:204-271).  One wave per (stream, head):
+// (submodules.py:204-271).  One 256-thread workgroup per (stream, group of 2 heads):
 //   recompute: q,k -> per-head LayerNorm(48) -> RoPE on dims [0,32) (q at positions 0..T-1, k at
 //              -S..T-1) -> scores = q.k^T / sqrt(48) -> mask (layers 14/15) -> softmax
 //   shared   : probabilities of the last recomputing layer (scores are shared and no mask applies
 //              to layers 1-6 / 8-13, so softmax(shared scores) = shared probabilities)
 //   ctx = P . V
+// LayerNorm+RoPE use 16 lanes per (row, head): lane l owns dims l, l+16 (a RoPE pair) and 32+l.
 constexpr int kMaxT = 10, kMaxTK = 40;
+constexpr int kHG = 2;                       // heads per workgroup
+constexpr int kHC = kHG * kDk;               // 96 columns per workgroup
+
 template <bool OBF>
-__global__ void __launch_bounds__(64) attention_kernel(AttnArgs a) {
-  __shared__ float qs[kMaxT][kDk + 1];
-  __shared__ float ks[kMaxTK][kDk + 1];
-  __shared__ float vs[kMaxTK][kDk + 1];
-  __shared__ float ps[kMaxT][kMaxTK + 1];
-  const int b = blockIdx.x / kHeads, h = blockIdx.x % kHeads, lane = threadIdx.x;
+__global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x / (kHeads / kHG), hg = blockIdx.x % (kHeads / kHG);
+  const int c0 = hg * kHC, tid = threadIdx.x;
   const int T = a.T, S = a.S, TK = S + T;
-  for (int i = lane; i < TK * kDk; i += 64) {
-    const int j = i / kDk, d = i % kDk;
-    vs[j][d] = a.v[((int64_t)b * TK + j) * a.ldv + h * kDk + d];
+  float* qs = sm;                    // [T][96]
+  float* ks = qs + T * kHC;          // [TK][96]
+  float* vs = ks + TK * kHC;         // [TK][96]
+  float* ps = vs + TK * kHC;         // [2][T][TK]
+  constexpr int C4 = kHC / 4;
+  for (int e = tid; e < TK * C4; e += 256) {
+    const int j = e / C4, c4 = e % C4;
+    *reinterpret_cast<float4*>(vs + j * kHC + 4 * c4) =
+        *reinterpret_cast<const float4*>(a.v + ((int64_t)b * TK + j) * a.ldv + c0 + 4 * c4);
   }
   if (a.recompute) {
-    for (int i = lane; i < T * kDk; i += 64) {
-      const int j = i / kDk, d = i % kDk;
-      qs[j][d] = a.q[((int64_t)b * T + j) * a.ldq + h * kDk + d];
+    for (int e = tid; e < T * C4; e += 256) {
+      const int j = e / C4, c4 = e % C4;
+      *reinterpret_cast<float4*>(qs + j * kHC + 4 * c4) =
+          *reinterpret_cast<const float4*>(a.q + ((int64_t)b * T + j) * a.ldq + c0 + 4 * c4);
     }
-    for (int i = lane; i < TK * kDk; i += 64) {
-      const int j = i / kDk, d = i % kDk;
-      ks[j][d] = a.k[((int64_t)b * TK + j) * a.ldk + h * kDk + d];
+    for (int e = tid; e < TK * C4; e += 256) {
+      const int j = e / C4, c4 = e % C4;
+      *reinterpret_cast<float4*>(ks + j * kHC + 4 * c4) =
+          *reinterpret_cast<const float4*>(a.k + ((int64_t)b * TK + j) * a.ldk + c0 + 4 * c4);
     }
     __syncthreads();
-    // LayerNorm + RoPE, one lane per row (rows: T query rows then TK key rows)
-    if (lane < T + TK) {
-      const bool isq = lane < T;
-      float* row = isq ? qs[lane] : ks[lane - T];
+    // per-head LayerNorm (eps 1e-5) + partial RoPE: 16 lanes per (row, head)
+    const int l = tid & 15;
+    const int npairs = (T + TK) * kHG;
+    for (int pr = tid >> 4; pr < ((npairs + 15) & ~15); pr += 16) {
+      const bool live = pr < npairs;
+      const int r = live ? pr / kHG : 0, hl = pr % kHG;
+      const bool isq = r < T;
+      float* base = (isq ? qs + r * kHC : ks + (r - T) * kHC) + hl * kDk;
       const float* lw = isq ? a.qln_w : a.kln_w;
       const float* lb = isq ? a.qln_b : a.kln_b;
-      const int pos = isq ? lane : (lane - T) - S;
-      float mu = 0.f;
-      for (int d = 0; d < kDk; ++d) mu += row[d];
-      mu /= (float)kDk;
-      float var = 0.f;
-      for (int d = 0; d < kDk; ++d) { const float c = row[d] - mu; var += c * c; }
+      const float x0 = base[l], x1 = base[l + 16], x2 = base[l + 32];
+      float sum = x0 + x1 + x2;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      const float mu = sum / (float)kDk;
+      const float d0 = x0 - mu, d1 = x1 - mu, d2 = x2 - mu;
+      float var = d0 * d0 + d1 * d1 + d2 * d2;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) var += __shfl_xor(var, o, 64);
       var /= (float)kDk;
       const float rstd = 1.0f / sqrtf(var + kLnEps);
-      for (int d = 0; d < kDk; ++d) row[d] = (row[d] - mu) * rstd * lw[d] + lb[d];
-      const float* cs = a.rope_cos + (pos + kMhsaS) * (kRope / 2);
-      const float* sn = a.rope_sin + (pos + kMhsaS) * (kRope / 2);
-      for (int d = 0; d < kRope / 2; ++d) {
-        const float x1 = row[d], x2 = row[d + kRope / 2];
-        row[d] = x1 * cs[d] - x2 * sn[d];
-        row[d + kRope / 2] = x2 * cs[d] + x1 * sn[d];
+      const float y0 = d0 * rstd * lw[l] + lb[l];
+      const float y1 = d1 * rstd * lw[l + 16] + lb[l + 16];
+      const float y2 = d2 * rstd * lw[l + 32] + lb[l + 32];
+      const int pos = isq ? r : (r - T) - S;
+      const float cs = a.rope_cos[(pos + kMhsaS) * (kRope / 2) + l];
+      const float sn = a.rope_sin[(pos + kMhsaS) * (kRope / 2) + l];
+      if (live) {
+        base[l] = y0 * cs - y1 * sn;            // rotate_half pairs (l, l+16), submodules.py:142-157
+        base[l + 16] = y1 * cs + y0 * sn;
+        base[l + 32] = y2;
       }
     }
     __syncthreads();
@@ -148,48 +168,71 @@ __global__ void __launch_bounds__(64) attention_kernel(AttnArgs a) {
       off = (float)kMhsaS - __half2float(a.s.in[a.s.row(b) + kOffMhsaLen]);
       if (a.reduced) off = floorf(off / 2.0f);
     }
-    for (int e = lane; e < T * TK; e += 64) {
-      const int i = e / TK, j = e % TK;
+    const int nsc = kHG * T * TK;
+    for (int e = tid; e < nsc; e += 256) {
+      const int hl = e / (T * TK), i = (e / TK) % T, j = e % TK;
+      const float4* q4 = reinterpret_cast<const float4*>(qs + i * kHC + hl * kDk);
+      const float4* k4 = reinterpret_cast<const float4*>(ks + j * kHC + hl * kDk);
       float acc = 0.f;
-      for (int d = 0; d < kDk; ++d) acc = fmaf(qs[i][d], ks[j][d], acc);
+#pragma unroll
+      for (int d = 0; d < kDk / 4; ++d) {
+        const float4 x = q4[d], y = k4[d];
+        acc = fmaf(x.x, y.x, acc);
+        acc = fmaf(x.y, y.y, acc);
+        acc = fmaf(x.z, y.z, acc);
+        acc = fmaf(x.w, y.w, acc);
+      }
       const float sc = acc / 6.928203230275509f;   // / math.sqrt(48) (submodules.py:185, conformer_blocks.py:725)
       const bool masked = (S > 0) && (((float)j < off) || ((float)(S + i) < off));
-      ps[i][j] = masked ? -10000.0f : sc;
+      ps[e] = masked ? -10000.0f : sc;
     }
     __syncthreads();
-    if (lane < T) {
-      const int i = lane;
+    for (int rr = tid; rr < kHG * T; rr += 256) {
+      float* row = ps + rr * TK;
+      const int i = rr % T;
       float m = -INFINITY;
-      for (int j = 0; j < TK; ++j) m = fmaxf(m, ps[i][j]);
+      for (int j = 0; j < TK; ++j) m = fmaxf(m, row[j]);
       float sum = 0.f;
-      for (int j = 0; j < TK; ++j) { const float e = expf(ps[i][j] - m); ps[i][j] = e; sum += e; }
+      for (int j = 0; j < TK; ++j) {
+        const float e = expf(row[j] - m);
+        row[j] = e;
+        sum += e;
+      }
       for (int j = 0; j < TK; ++j) {
         const bool masked = (S > 0) && (((float)j < off) || ((float)(S + i) < off));
-        ps[i][j] = masked ? 0.f : ps[i][j] / sum;
+        row[j] = masked ? 0.f : row[j] / sum;
       }
     }
     __syncthreads();
     if (a.probs) {
-      for (int e = lane; e < T * TK; e += 64)
-        a.probs[(((int64_t)b * kHeads + h) * T + e / TK) * TK + e % TK] = ps[e / TK][e % TK];
+      for (int e = tid; e < kHG * T * TK; e += 256) {
+        const int hl = e / (T * TK), rem = e % (T * TK);
+        a.probs[(((int64_t)b * kHeads + hg * kHG + hl) * T) * TK + rem] = ps[e];
+      }
     }
   } else {
-    for (int e = lane; e < T * TK; e += 64)
-      ps[e / TK][e % TK] = a.probs[(((int64_t)b * kHeads + h) * T + e / TK) * TK + e % TK];
+    for (int e = tid; e < kHG * T * TK; e += 256) {
+      const int hl = e / (T * TK), rem = e % (T * TK);
+      ps[e] = a.probs[(((int64_t)b * kHeads + hg * kHG + hl) * T) * TK + rem];
+    }
     __syncthreads();
   }
-  for (int e = lane; e < T * kDk; e += 64) {
-    const int i = e / kDk, d = e % kDk;
+  for (int e = tid; e < T * kHC; e += 256) {
+    const int i = e / kHC, c = e % kHC, hl = c / kDk;
+    const float* pr = ps + (hl * T + i) * TK;
     float acc = 0.f;
-    for (int j = 0; j < TK; ++j) acc = fmaf(ps[i][j], vs[j][d], acc);
-    store_act<OBF>(a.ctx, ((int64_t)b * T + i) * kD + h * kDk + d, acc);
+    for (int j = 0; j < TK; ++j) acc = fmaf(pr[j], vs[j * kHC + c], acc);
+    store_act<OBF>(a.ctx, ((int64_t)b * T + i) * kD + c0 + c, acc);
   }
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if (a.T > kMaxT || a.S + a.T > kMaxTK) return hipErrorInvalidValue;
-  if (a.ctx_bf16) hipLaunchKernelGGL(attention_kernel<true>, dim3(a.B * kHeads), dim3(64), 0, st, a);
-  else hipLaunchKernelGGL(attention_kernel<false>, dim3(a.B * kHeads), dim3(64), 0, st, a);
+  const int tk = a.S + a.T;
+  const size_t smem = (size_t)(a.T * kHC + 2 * tk * kHC + kHG * a.T * tk) * sizeof(float);
+  const dim3 grid(a.B * (kHeads / kHG));
+  if (a.ctx_bf16) hipLaunchKernelGGL(attention_kernel<true>, grid, dim3(256), smem, st, a);
+  else hipLaunchKernelGGL(attention_kernel<false>, grid, dim3(256), smem, st, a);
   return hipGetLastError();
 }
 
@@ -197,42 +240,89 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
 // ConformerConvolution depthwise part (conformer_blocks.py:427-433, submodules.py:364-402):
 //   x = [conv state (30) ; g (T)] per channel; next state = x[-30:]
 //   out[t] = SiLU(BN(bias + sum_k w[k] x[t+k]))  with BN folded into (w, b) on the host.
-// One thread per (stream, channel).
+// One 384-thread workgroup (a thread per channel) handles kDwStreams streams with the channel's 31 taps
+// (stored tap-major) in registers.  Each stream's 23 KB conv-state section is moved HBM<->LDS in 16-byte
+// vectors: state rows are only 2-byte aligned, so the section is read from the enclosing 16-byte-aligned
+// window (the section is interior to the row) and the two partial end vectors are written element-wise.
+constexpr int kDwStreams = 2;
+constexpr int kDwSec = kD * kConvS;          // 11520 halves per (stream, layer)
+constexpr int kDwVec = kDwSec / 8 + 1;       // 16-byte vectors covering a misaligned section
 template <int T, bool OBF>
-__global__ void __launch_bounds__(256) dwconv_kernel(const float* __restrict__ g, StateRef s, int layer,
-                                                     const float* __restrict__ w, const float* __restrict__ bias,
-                                                     void* __restrict__ out, int B) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= B * kD) return;
-  const int b = idx / kD, c = idx % kD;
-  const int64_t st = s.row(b) + kOffConv + ((int64_t)layer * kD + c) * kConvS;
-  float x[kConvS + T];
+__global__ void __launch_bounds__(kD) dwconv_kernel(const float* __restrict__ g, StateRef s, int layer,
+                                                    const float* __restrict__ w, const float* __restrict__ bias,
+                                                    void* __restrict__ out, int B) {
+  __shared__ uint4 lds[kDwStreams][kDwVec];
+  const int c = threadIdx.x;
+  int shift[kDwStreams], nvec[kDwStreams];
+  int64_t base[kDwStreams];
 #pragma unroll
-  for (int i = 0; i < kConvS; ++i) x[i] = __half2float(s.in[st + i]);
-#pragma unroll
-  for (int t = 0; t < T; ++t) x[kConvS + t] = g[((int64_t)b * T + t) * kD + c];
+  for (int si = 0; si < kDwStreams; ++si) {
+    const int b = min(blockIdx.x * kDwStreams + si, B - 1);
+    base[si] = s.row(b) + kOffConv + (int64_t)layer * kDwSec;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(s.in + base[si]);
+    shift[si] = (int)((a & 15) >> 1);
+    nvec[si] = (shift[si] + kDwSec + 7) >> 3;
+    const uint4* q = reinterpret_cast<const uint4*>(a & ~uintptr_t(15));
+    for (int v = c; v < nvec[si]; v += kD) lds[si][v] = q[v];
+  }
   float wr[kConvK];
 #pragma unroll
-  for (int k = 0; k < kConvK; ++k) wr[k] = w[c * kConvK + k];
+  for (int k = 0; k < kConvK; ++k) wr[k] = w[k * kD + c];
   const float bb = bias[c];
+  __syncthreads();
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    float acc = bb;
+  for (int si = 0; si < kDwStreams; ++si) {
+    const int b = blockIdx.x * kDwStreams + si;
+    if (b >= B) break;
+    __half* h = reinterpret_cast<__half*>(lds[si]) + shift[si] + c * kConvS;
+    float x[kConvS + T];
 #pragma unroll
-    for (int k = 0; k < kConvK; ++k) acc = fmaf(wr[k], x[t + k], acc);
-    store_act<OBF>(out, ((int64_t)b * T + t) * kD + c, silu_f(acc));
+    for (int t = 0; t < T; ++t) x[kConvS + t] = g[((int64_t)b * T + t) * kD + c];
+#pragma unroll
+    for (int i = 0; i < kConvS; ++i) x[i] = __half2float(h[i]);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      float acc = bb;
+#pragma unroll
+      for (int k = 0; k < kConvK; ++k) acc = fmaf(wr[k], x[t + k], acc);
+      store_act<OBF>(out, ((int64_t)b * T + t) * kD + c, silu_f(acc));
+    }
+#pragma unroll
+    for (int i = 0; i < kConvS; ++i) h[i] = __float2half_rn(x[T + i]);
   }
+  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < kConvS; ++i) s.out[st + i] = __float2half_rn(x[T + i]);
+  for (int si = 0; si < kDwStreams; ++si) {
+    const int b = blockIdx.x * kDwStreams + si;
+    if (b >= B) break;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(s.out + base[si]);
+    const int sh = (int)((a & 15) >> 1);
+    __half* dst = s.out + base[si];
+    const __half* src = reinterpret_cast<const __half*>(lds[si]) + shift[si];
+    if (sh == shift[si]) {
+      uint4* q = reinterpret_cast<uint4*>(a & ~uintptr_t(15));
+      const int n = nvec[si];
+      for (int v = c; v < n; v += kD) {
+        if ((v == 0 && sh) || (v == n - 1 && ((sh + kDwSec) & 7))) {
+          const int e0 = v * 8 - sh;
+          for (int e = max(e0, 0); e < min(e0 + 8, kDwSec); ++e) dst[e] = src[e];
+        } else {
+          q[v] = lds[si][v];
+        }
+      }
+    } else {  // output slab aligned differently from the input slab
+      for (int e = c; e < kDwSec; e += kD) dst[e] = src[e];
+    }
+  }
 }
 
 hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
                          int T, int B, hipStream_t st) {
-  const dim3 grid((B * kD + 255) / 256);
-  if (T == kT && obf) hipLaunchKernelGGL((dwconv_kernel<kT, true>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
-  else if (T == kT) hipLaunchKernelGGL((dwconv_kernel<kT, false>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
-  else if (T == kT / 2 && obf) hipLaunchKernelGGL((dwconv_kernel<kT / 2, true>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
-  else if (T == kT / 2) hipLaunchKernelGGL((dwconv_kernel<kT / 2, false>), grid, dim3(256), 0, st, g, s, layer, w, b, out, B);
+  const dim3 grid((B + kDwStreams - 1) / kDwStreams), block(kD);
+  if (T == kT && obf) hipLaunchKernelGGL((dwconv_kernel<kT, true>), grid, block, 0, st, g, s, layer, w, b, out, B);
+  else if (T == kT) hipLaunchKernelGGL((dwconv_kernel<kT, false>), grid, block, 0, st, g, s, layer, w, b, out, B);
+  else if (T == kT / 2 && obf) hipLaunchKernelGGL((dwconv_kernel<kT / 2, true>), grid, block, 0, st, g, s, layer, w, b, out, B);
+  else if (T == kT / 2) hipLaunchKernelGGL((dwconv_kernel<kT / 2, false>), grid, block, 0, st, g, s, layer, w, b, out, B);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -41,9 +41,11 @@ hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, h
 //   c1[c][t][f] = SiLU(BN(bias + sum_{kt<11,kf<21} w[c][kt][kf] x1[t+kt][f+kf])), t<30, f<44
 //   x2 = [sub2 state (8 rows) ; c1] written channels-last [38][44][32] for the conv2 implicit GEMM;
 //   next sub2 = c1[:, 22:30, :].
-// One workgroup per stream.  The conv is an implicit GEMM on the fp32 MFMA: M = 1320 positions
-// (32-row tiles per wave), N = 32 channels, K = 231 taps padded to 256, A gathered from x1 in LDS.
+// One workgroup per stream.  The conv is an implicit GEMM on the MFMA (fp32, or bf16 in bf16 mode):
+// M = 1320 positions (32-row tiles per wave), N = 32 channels, K = 231 taps padded to 256, A gathered
+// from x1 in LDS.
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 constexpr int kK1 = kSub1Kt * kSub1Kf;      // 231
 constexpr int kK1P = 256;                   // padded K
 constexpr int kPos1 = kMelT * kSub1F;       // 1320
@@ -90,10 +92,25 @@ __global__ void __launch_bounds__(256) sub1_kernel(const float* __restrict__ fea
     f32x16_t acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if constexpr (OBF) {
+      // bf16 mode: v_mfma_f32_32x32x16_bf16, lane (i, h) holds A[pos_i][16s + 8h + e] (gathered)
+#pragma unroll 4
+      for (int st = 0; st < kK1P / 16; ++st) {
+        bf16x8_t av, bv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 16 * st + 8 * lh + e;
+          av[e] = (__bf16)x1[base + koff[k]];
+          bv[e] = (__bf16)wk[li][k];
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+      }
+    } else {
 #pragma unroll 8
-    for (int st = 0; st < kK1P / 2; ++st) {
-      const int k = 2 * st + lh;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[base + koff[k]], wk[li][k], acc, 0, 0, 0);
+      for (int st = 0; st < kK1P / 2; ++st) {
+        const int k = 2 * st + lh;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[base + koff[k]], wk[li][k], acc, 0, 0, 0);
+      }
     }
     const int c = li;
 #pragma unroll

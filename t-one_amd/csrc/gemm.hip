@@ -52,20 +52,51 @@ __device__ __forceinline__ uint16_t bf16_bits(float a) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+template <class T>
+__device__ __forceinline__ void st_out(T* ptr, T v, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, ptr);
+  else *ptr = v;
+}
+
 template <int BM_, int BN_, int WM_, int WN_>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
 };
 
 // Shared epilogue.  C/D map of v_mfma_*_32x32: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+// Every operand the epilogue reads (bias, BN scale/shift, residual rows) is loaded into registers
+// before the first store: C may alias R, so a load placed after a store could not be hoisted and
+// each one would pay a full memory latency in series.
 template <class TL, int EPI, bool CBF, bool SPLIT, int TM = TL::BM / TL::WM / 32, int TN = TL::BN / TL::WN / 32>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[TM][TN], const float* rden, int m0, int n0,
                                               int wm, int wn, int lane) {
   constexpr int WTM = TL::BM / TL::WM, WTN = TL::BN / TL::WN;
   constexpr bool CONV2 = (EPI == EPI_CONV2);
+  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU || EPI == EPI_POWER);
   const int lr = lane & 31, lh = lane >> 5;
+  const int cbase = n0 + wn * WTN + lr;          // column of n-tile j: cbase + 32 j
+  const bool nt = p.nt_store;
+  float bcol[TN], scol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    bcol[j] = 0.f;
+    scol[j] = 1.f;
+    if constexpr (!SPLIT && EPI != EPI_POWER && EPI != EPI_LOGMEL) {
+      if (p.bias) bcol[j] = p.bias[cbase + j * 32];
+      if constexpr (CONV2) scol[j] = p.scale[cbase + j * 32];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    float rres[16][TN];
+    if constexpr (EPI == EPI_RESID && !SPLIT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = min(m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rres[r][j] = p.R[(int64_t)row * p.ldr + cbase + j * 32];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int lrow = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -74,22 +105,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[T
       if constexpr (SPLIT) {
         float* dst = p.ws + ((int64_t)blockIdx.y * p.M + row) * p.N;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 32 + lr] = acc[i][j][r];
+        for (int j = 0; j < TN; ++j) dst[cbase + j * 32] = acc[i][j][r];
       } else if constexpr (CONV2) {
         const int b = row / (kT * kSub2F), rem = row % (kT * kSub2F);
         const int t = rem / kSub2F, f = rem % kSub2F;
         const int64_t o = ((int64_t)b * kT + t) * kSubOut + f * kSub2C;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int c = n0 + wn * WTN + j * 32 + lr;
-          const float y = silu_f(fmaf(acc[i][j][r], p.scale[c], p.bias[c]));
+          const int c = cbase + j * 32;
+          const float y = silu_f(fmaf(acc[i][j][r], scol[j], bcol[j]));
           if constexpr (CBF) static_cast<uint16_t*>(p.C)[o + c] = bf16_bits(y);
           else static_cast<float*>(p.C)[o + c] = y;
         }
       } else if constexpr (EPI == EPI_LOGMEL) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int col = n0 + wn * WTN + j * 32 + lr;
+          const int col = cbase + j * 32;
           if (col < p.n_out)
             static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = round_h(logf(acc[i][j][r] + 5.9604644775390625e-08f));
         }
@@ -97,20 +128,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[T
         const float den = p.rowscale ? rden[lrow] : 1.0f;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int col = n0 + wn * WTN + j * 32 + lr;
+          const int col = cbase + j * 32;
           float v = acc[i][j][r];
           if (p.rowscale) v = v / den;
-          if (p.bias) v += p.bias[col];
-          if constexpr (EPI == EPI_RESID) v = p.R[(int64_t)row * p.ldr + col] + p.alpha * v;
-          if constexpr (CBF) static_cast<uint16_t*>(p.C)[(int64_t)row * p.ldc + col] = bf16_bits(v);
-          else static_cast<float*>(p.C)[(int64_t)row * p.ldc + col] = v;
-          if (p.C2) p.C2[(int64_t)row * p.ldc + col] = bf16_bits(v);   // bf16 shadow of the residual
+          v += bcol[j];
+          if constexpr (EPI == EPI_RESID) v = rres[r][j] + p.alpha * v;
+          if constexpr (CBF) st_out(static_cast<uint16_t*>(p.C) + (int64_t)row * p.ldc + col, bf16_bits(v), nt);
+          else st_out(static_cast<float*>(p.C) + (int64_t)row * p.ldc + col, v, nt);
+          if (p.C2) st_out(p.C2 + (int64_t)row * p.ldc + col, bf16_bits(v), nt);   // bf16 shadow of the residual
         }
       } else {
+        static_assert(PAIRED, "unhandled epilogue");
         const float den = p.rowscale ? rden[lrow] : 1.0f;
 #pragma unroll
         for (int jp = 0; jp < TN / 2; ++jp) {
-          const int cg = n0 + wn * WTN + 2 * jp * 32 + lr;   // packed column of the first member
           float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
           const int oc = (n0 + wn * WTN) / 2 + jp * 32 + lr;
           float o;
@@ -118,16 +149,98 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[T
             o = g * g + u * u;
           } else {
             if (p.rowscale) { g = g / den; u = u / den; }
-            g += p.bias[cg];
-            u += p.bias[cg + 32];
+            g += bcol[2 * jp];
+            u += bcol[2 * jp + 1];
             if constexpr (EPI == EPI_SWIGLU) o = silu_f(g) * u;   // linear1 -> SiLU, times linearv
             else o = g * sigmoid_f(u);                            // GLU: first half * sigmoid(second)
           }
-          if constexpr (CBF) static_cast<uint16_t*>(p.C)[(int64_t)row * p.ldc + oc] = bf16_bits(o);
-          else static_cast<float*>(p.C)[(int64_t)row * p.ldc + oc] = o;
+          if constexpr (CBF) st_out(static_cast<uint16_t*>(p.C) + (int64_t)row * p.ldc + oc, bf16_bits(o), nt);
+          else st_out(static_cast<float*>(p.C) + (int64_t)row * p.ldc + oc, o, nt);
         }
       }
     }
+  }
+}
+
+// LDS-staged epilogue (LDS-DMA kernel): the wave tiles go to LDS as fp32 in the MFMA layout (the
+// stage buffers are free after the K loop), then the block writes whole output rows with 16-byte
+// fp32 / 8-byte bf16 vectors, so each 128-byte line leaves in one instruction instead of as 64-byte
+// halves from two waves, and residual rows are read as vectors (all before the first store).
+template <class TL, int EPI, bool CBF, bool SPLIT, int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&acc)[TM][TN], const float* rden, float* Cs,
+                                                  int m0, int n0, int wm, int wn, int tid) {
+  constexpr int NT = TL::WM * TL::WN * 64;
+  constexpr int WTM = TL::BM / TL::WM, WTN = TL::BN / TL::WN;
+  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
+  static_assert(PAIRED || EPI == EPI_STORE || EPI == EPI_RESID, "LDS epilogue: STORE/RESID/SWIGLU/GLU");
+  constexpr int BNO = PAIRED ? TL::BN / 2 : TL::BN;
+  const int lane = tid & 63, lr = lane & 31, lh = lane >> 5;
+  float bcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bcol[j] = (!SPLIT && p.bias) ? p.bias[n0 + wn * WTN + j * 32 + lr] : 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lrow = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const float den = (!SPLIT && p.rowscale) ? rden[lrow] : 1.0f;
+      if constexpr (PAIRED) {
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp) {
+          float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
+          if (p.rowscale) { g = g / den; u = u / den; }
+          g += bcol[2 * jp];
+          u += bcol[2 * jp + 1];
+          const float o = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);
+          Cs[lrow * BNO + (wn * WTN) / 2 + jp * 32 + lr] = o;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v = acc[i][j][r];
+          if constexpr (!SPLIT) {
+            if (p.rowscale) v = v / den;
+            v += bcol[j];
+          }
+          Cs[lrow * BNO + wn * WTN + j * 32 + lr] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int RV = BNO / 4;                 // 4-float vectors per row
+  constexpr int NV = TL::BM * RV / NT;        // vectors per thread
+  static_assert(NV >= 1 && (TL::BM * RV) % NT == 0, "tile/thread mismatch");
+  const int ocol0 = PAIRED ? n0 / 2 : n0;
+  f32x4 val[NV], res[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * NT, row = q / RV, c = (q % RV) * 4;
+    val[k] = *reinterpret_cast<const f32x4*>(Cs + row * BNO + c);
+    if constexpr (EPI == EPI_RESID && !SPLIT) {
+      const int grow = min(m0 + row, p.M - 1);
+      res[k] = *reinterpret_cast<const f32x4*>(p.R + (int64_t)grow * p.ldr + ocol0 + c);
+    }
+  }
+  const bool nt = p.nt_store;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * NT, row = q / RV, c = (q % RV) * 4;
+    const int grow = m0 + row;
+    if (grow >= p.M) continue;
+    f32x4 v = val[k];
+    if constexpr (SPLIT) {
+      st_out(reinterpret_cast<f32x4*>(p.ws + ((int64_t)blockIdx.y * p.M + grow) * p.N + n0 + c), v, nt);
+      continue;
+    }
+    if constexpr (EPI == EPI_RESID) v = res[k] + p.alpha * v;
+    const int64_t o = (int64_t)grow * p.ldc + ocol0 + c;
+    u32x2 h;
+    h.x = pack_bf16x2(v.x, v.y);
+    h.y = pack_bf16x2(v.z, v.w);
+    if constexpr (CBF) st_out(reinterpret_cast<u32x2*>(static_cast<uint16_t*>(p.C) + o), h, nt);
+    else st_out(reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + o), v, nt);
+    if (p.C2) st_out(reinterpret_cast<u32x2*>(p.C2 + o), h, nt);
   }
 }
 
@@ -344,7 +457,12 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
 // A rowscale GEMM reads the bf16 shadow of the residual and takes each row's sum of squares from
 // its own A fragments (waves of the first N column only).
 // Split-K is a runtime mode here (p.k_split > 0: K slice blockIdx.y, raw partials to p.ws).
-template <class TL, int EPI, bool CBF>
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <class TL, int EPI, bool CBF, int S>
 __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArgs p) {
   constexpr int BM = TL::BM, BN = TL::BN, WM = TL::WM, WN = TL::WN;
   constexpr int kNWaves = WM * WN;
@@ -355,18 +473,26 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
   constexpr int A_I = BM / 8 / kNWaves, W_I = BN / 8 / kNWaves;     // DMA wave-instructions per K-step
   static_assert(A_I >= 1 && W_I >= 1 && BM % (8 * kNWaves) == 0 && BN % (8 * kNWaves) == 0, "tile/wave mismatch");
   constexpr int kStageElems = (BM + BN) * BK;                    // bf16 elements per buffer
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kStageElems + 2 * BM];   // one LDS object (+ rden)
-  float* rden = reinterpret_cast<float*>(lds + 2 * kStageElems);
+  static_assert(S >= 2 && S <= 4, "2..4 LDS stages");
+  constexpr int kIps = A_I + W_I;                                // DMA instructions per stage per thread
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * kStageElems + 2 * BM];   // one LDS object (+ rden)
+  float* rden = reinterpret_cast<float*>(lds + S * kStageElems);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = p.N / BN;
-  int wgid = blockIdx.x;
-  {
-    const int nwg = gridDim.x, xcd = wgid & 7, q = nwg >> 3, rr = nwg & 7;
-    wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
+  int bm, bn;
+  if (p.order_n && (ntn & 7) == 0) {
+    // large W: each XCD keeps an eighth of W's rows hot in its L2 and walks every M-tile
+    const int npx = ntn >> 3, li = blockIdx.x >> 3;
+    bm = li / npx;
+    bn = (blockIdx.x & 7) * npx + li % npx;
+  } else {
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (blockIdx.x >> 3);
+    bm = wgid / ntn;
+    bn = wgid % ntn;
   }
-  const int bm = wgid / ntn, bn = wgid % ntn;
   const int m0 = bm * BM, n0 = bn * BN;
   const bool split = p.k_split > 0;
   const int kb = split ? (int)blockIdx.y * p.k_split : 0;
@@ -464,6 +590,11 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
             ss[i] = fmaf(v, v, ss[i]);
           }
       }
+      if (p.dbg & 2) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][0][0] += (float)a[i][0] + (float)b[0][i & 1];
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -471,16 +602,21 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
     }
   };
 
-  stage(0, kb);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kb + (kt + 1) * BK);
-    compute(cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // S-deep ring: stages kt+1 .. kt+S-2 stay in flight while stage kt is consumed; one barrier per
+  // K-step both publishes stage kt and frees buffer (kt-1) % S for the DMA of stage kt+S-1.
+#pragma unroll
+  for (int s0 = 0; s0 < S - 1; ++s0)
+    if (s0 < nk) stage(s0, kb + s0 * BK);
+  for (int kt = 0; kt < ((p.dbg & 4) ? 0 : nk); ++kt) {
+    const int ahead = min(S - 2, nk - 1 - kt);      // younger stages allowed to remain in flight
+    if (S >= 4 && ahead >= 2) wait_vmcnt<(S >= 4 ? 2 * kIps : 0)>();
+    else if (S >= 3 && ahead >= 1) wait_vmcnt<(S >= 3 ? kIps : 0)>();
+    else wait_vmcnt<0>();
     __syncthreads();
+    if (kt + S - 1 < nk) stage((kt + S - 1) % S, kb + (kt + S - 1) * BK);
+    compute(kt % S);
   }
+  __syncthreads();
 
   if (p.rowscale) {
     if (want_ss) {
@@ -498,6 +634,23 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
       }
     }
     __syncthreads();
+  }
+  if (p.dbg & 1) {
+    if (acc[0][0][0] == 1234.5f) static_cast<float*>(p.C)[tid] = acc[TM - 1][TN - 1][15];
+    return;
+  }
+  constexpr bool kLdsEpi = (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU || EPI == EPI_GLU) &&
+                           BM * BN * 4 <= S * kStageElems * 2;
+  if constexpr (kLdsEpi) {
+    float* Cs = reinterpret_cast<float*>(lds);
+    if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+      if (split) {
+        gemm_epilogue_lds<TL, EPI_STORE, false, true>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
+        return;
+      }
+    }
+    gemm_epilogue_lds<TL, EPI, CBF, false>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
+    return;
   }
   if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
     if (split) {
@@ -582,15 +735,16 @@ static hipError_t launch_prec(const GemmArgs& a, int epi, bool bf16, int nsplit,
   return a.c_bf16 ? launch_epi<TL, true, false, true>(a, epi, nsplit, st) : launch_epi<TL, true, false, false>(a, epi, nsplit, st);
 }
 
-template <class TL, int EPI, bool CBF>
+template <class TL, int EPI, bool CBF, int S = 2>
 static hipError_t launch_glds(const GemmArgs& a, int nsplit, hipStream_t st) {
+  if (a.N % TL::BN || (nsplit > 1 && (a.K % (nsplit * 64)))) return hipErrorInvalidValue;
   const int tiles = ((a.M + TL::BM - 1) / TL::BM) * (a.N / TL::BN);
   const dim3 block(TL::WM * TL::WN * 64);
   if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
     if (nsplit > 1) {
       GemmArgs b = a;
       b.k_split = a.K / nsplit;
-      hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI_STORE, false>), dim3(tiles, nsplit), block, 0, st, b);
+      hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI_STORE, false, S>), dim3(tiles, nsplit), block, 0, st, b);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       const int64_t n4 = (int64_t)a.M * (a.N / 4);
@@ -601,17 +755,17 @@ static hipError_t launch_glds(const GemmArgs& a, int nsplit, hipStream_t st) {
   }
   GemmArgs c = a;
   c.k_split = 0;
-  hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI, CBF>), dim3(tiles), block, 0, st, c);
+  hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI, CBF, S>), dim3(tiles), block, 0, st, c);
   return hipGetLastError();
 }
 
-template <class TL>
+template <class TL, int S = 2>
 static hipError_t launch_glds_epi(const GemmArgs& a, int epi, int nsplit, hipStream_t st) {
   switch (epi) {
-    case EPI_STORE: return a.c_bf16 ? launch_glds<TL, EPI_STORE, true>(a, nsplit, st) : launch_glds<TL, EPI_STORE, false>(a, nsplit, st);
-    case EPI_RESID: return launch_glds<TL, EPI_RESID, false>(a, nsplit, st);
-    case EPI_SWIGLU: return a.c_bf16 ? launch_glds<TL, EPI_SWIGLU, true>(a, 1, st) : launch_glds<TL, EPI_SWIGLU, false>(a, 1, st);
-    case EPI_GLU: return a.c_bf16 ? launch_glds<TL, EPI_GLU, true>(a, 1, st) : launch_glds<TL, EPI_GLU, false>(a, 1, st);
+    case EPI_STORE: return a.c_bf16 ? launch_glds<TL, EPI_STORE, true, S>(a, nsplit, st) : launch_glds<TL, EPI_STORE, false, S>(a, nsplit, st);
+    case EPI_RESID: return launch_glds<TL, EPI_RESID, false, S>(a, nsplit, st);
+    case EPI_SWIGLU: return a.c_bf16 ? launch_glds<TL, EPI_SWIGLU, true, S>(a, 1, st) : launch_glds<TL, EPI_SWIGLU, false, S>(a, 1, st);
+    case EPI_GLU: return a.c_bf16 ? launch_glds<TL, EPI_GLU, true, S>(a, 1, st) : launch_glds<TL, EPI_GLU, false, S>(a, 1, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -634,6 +788,23 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   }
   if (nsplit > 1 || t64 >= kTarget / 2) return launch_glds_epi<Tile<64, 128, 2, 2>>(a, epi, nsplit, st);
   return launch_glds_epi<Tile<32, 128, 1, 2>>(a, epi, 1, st);
+}
+
+// Fixed bf16 tile/stage variants (tools/gemm_bench.hip), bypassing the size heuristics.
+hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st) {
+  switch (variant) {
+    case 0: return launch_glds_epi<Tile<128, 128, 2, 2>, 2>(a, epi, nsplit, st);
+    case 1: return launch_glds_epi<Tile<128, 128, 2, 2>, 3>(a, epi, nsplit, st);
+    case 2: return launch_glds_epi<Tile<128, 128, 2, 2>, 4>(a, epi, nsplit, st);
+    case 3: return launch_glds_epi<Tile<256, 128, 4, 2>, 2>(a, epi, nsplit, st);
+    case 4: return launch_glds_epi<Tile<256, 128, 4, 2>, 3>(a, epi, nsplit, st);
+    case 5: return launch_glds_epi<Tile<128, 256, 2, 4>, 2>(a, epi, nsplit, st);
+    case 6: return launch_glds_epi<Tile<256, 256, 2, 4>, 2>(a, epi, nsplit, st);
+    case 7: return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, nsplit, st);
+    case 8: return launch_glds_epi<Tile<64, 128, 2, 2>, 3>(a, epi, nsplit, st);
+    case 9: return launch_glds_epi<Tile<64, 128, 2, 2>, 4>(a, epi, nsplit, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
@@ -676,7 +847,7 @@ hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const f
   a.N = kSub2C;
   a.K = bf16 ? kConv2KPad : kSub2Kt * kSub2Kf * kSub1C;
   const dim3 grid((a.M + 127) / 128), block(256);
-  if (bf16) hipLaunchKernelGGL((gemm_glds_kernel<Tile<128, 64, 4, 1>, EPI_CONV2, true>), grid, block, 0, st, a);
+  if (bf16) hipLaunchKernelGGL((gemm_glds_kernel<Tile<128, 64, 4, 1>, EPI_CONV2, true, 2>), grid, block, 0, st, a);
   else hipLaunchKernelGGL((gemm_kernel<Tile<128, 64, 4, 1>, EPI_CONV2, false, false, false, false>), grid, block, 0, st, a);
   return hipGetLastError();
 }

@@ -35,9 +35,14 @@ struct GemmArgs {
   int64_t gstride;
   int n_out;          // EPI_LOGMEL: columns written
   uint16_t* C2;       // STORE/RESID: optional bf16 shadow of C (same ldc), feeds bf16 GEMMs
+  int order_n;        // bf16 LDS-DMA kernel: XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8) (large W)
+  int nt_store;       // non-temporal epilogue stores
+  int dbg;            // microbenchmark only: 1 = no epilogue, 2 = no MFMA, 4 = no K loop
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
+// bf16 operands, fixed tile/stage variant (microbenchmarks)
+hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 
 // a3 conv2 as an implicit GEMM over all streams: A rows gathered from the channels-last
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,

@@ -57,7 +57,7 @@ struct LayerW {
   float* bo;
   void* wpw1;         // [768][384] GLU-interleaved, norm folded
   float* bpw1;
-  float* wdw;         // [384][31] BN folded
+  float* wdw;         // [31][384] BN folded, tap-major
   float* bdw;
   void* wpw2;
   float* bpw2;
@@ -618,7 +618,7 @@ int finalize_weights(tone_session* s) {
     std::vector<float> wd((size_t)D * kConvK), bd(D);
     for (int ch = 0; ch < D; ++ch) {
       const double scale = (double)(*bn[0])[ch] / std::sqrt((double)(*bn[3])[ch] + 1e-5);
-      for (int k = 0; k < kConvK; ++k) wd[(size_t)ch * kConvK + k] = (float)((double)(*dww)[(size_t)ch * kConvK + k] * scale);
+      for (int k = 0; k < kConvK; ++k) wd[(size_t)k * D + ch] = (float)((double)(*dww)[(size_t)ch * kConvK + k] * scale);
       bd[ch] = (float)(((double)(*dwb)[ch] - (double)(*bn[2])[ch]) * scale + (double)(*bn[1])[ch]);
     }
     CALL(upload(s, &lw.wdw, wd));

@@ -1,0 +1,126 @@
+// Microbenchmark + self-check of the bf16 GEMM tile/stage variants at the encoder's shapes.
+//   gemm_bench M K N epi variants [nsplit] [iters]      (epi: 0 STORE 1 RESID 2 SWIGLU 3 GLU)
+// Prints one JSON line per variant: average launch time, TFLOP/s and max |err| against a naive
+// fp32-accumulate kernel on the same bf16 operands.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "../kernels.h"
+
+using namespace tone;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+static uint16_t to_bf16(float f) {
+  uint32_t u; memcpy(&u, &f, 4);
+  u += 0x7fff + ((u >> 16) & 1);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ float bf(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+// naive reference: out[m][o] for the epilogue (no rowscale)
+__global__ void ref_kernel(const uint16_t* A, const uint16_t* W, const float* bias, const float* R, float* out, int M,
+                           int N, int K, int epi) {
+  const int m = blockIdx.y, o = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nout = (epi >= 2) ? N / 2 : N;
+  if (o >= nout) return;
+  auto dot = [&](int n) {
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc += bf(A[(int64_t)m * K + k]) * bf(W[(int64_t)n * K + k]);
+    return acc + bias[n];
+  };
+  float v;
+  if (epi <= 1) {
+    v = dot(o);
+    if (epi == 1) v = R[(int64_t)m * N + o] + v;
+  } else {
+    const int blk = o / 32, c = o % 32, n0 = blk * 64 + c;
+    const float g = dot(n0), u = dot(n0 + 32);
+    v = (epi == 2) ? g / (1.f + expf(-g)) * u : g / (1.f + expf(-u));
+  }
+  out[(int64_t)m * nout + o] = v;
+}
+
+__global__ void err_kernel(const void* C, int cbf, const float* ref, int64_t n, float* err) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float e = 0.f;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float c = cbf ? bf(static_cast<const uint16_t*>(C)[i]) : static_cast<const float*>(C)[i];
+    const float r = ref[i];
+    e = fmaxf(e, fabsf(c - r) / (1.f + fabsf(r)));
+  }
+  atomicMax(reinterpret_cast<int*>(err), __float_as_int(e));
+}
+
+int main(int argc, char** argv) {
+  if (argc < 6) { fprintf(stderr, "usage: %s M K N epi v1,v2,.. [nsplit] [iters]\n", argv[0]); return 2; }
+  const int M = atoi(argv[1]), K = atoi(argv[2]), N = atoi(argv[3]), epi = atoi(argv[4]);
+  const int nsplit = argc > 6 ? atoi(argv[6]) : 1, iters = argc > 7 ? atoi(argv[7]) : 20;
+  const int nout = epi >= 2 ? N / 2 : N;
+  const int cbf = epi >= 2 ? 1 : 0;   // as in the session: qkv/attn fp32, SWIGLU/GLU bf16
+  std::vector<uint16_t> hA((size_t)M * K), hW((size_t)N * K);
+  std::vector<float> hb(N), hR((size_t)M * N);
+  uint64_t x = 12345;
+  auto rnd = [&]() { x = x * 6364136223846793005ull + 1442695040888963407ull; return (float)((x >> 40) & 0xffffff) / 16777216.f * 2.f - 1.f; };
+  for (auto& v : hA) v = to_bf16(rnd());
+  for (auto& v : hW) v = to_bf16(rnd() * 0.05f);
+  for (auto& v : hb) v = rnd() * 0.1f;
+  for (auto& v : hR) v = rnd();
+  uint16_t *A, *W, *C2;
+  float *bias, *R, *ref, *err, *ws;
+  void* C;
+  CK(hipMalloc(&A, hA.size() * 2)); CK(hipMalloc(&W, hW.size() * 2));
+  CK(hipMalloc(&bias, N * 4)); CK(hipMalloc(&R, hR.size() * 4));
+  CK(hipMalloc(&C, (size_t)M * nout * 4)); CK(hipMalloc(&C2, (size_t)M * nout * 2));
+  CK(hipMalloc(&ref, (size_t)M * nout * 4)); CK(hipMalloc(&err, 4));
+  const int64_t ws_cap = (int64_t)16 * M * N;
+  CK(hipMalloc(&ws, ws_cap * 4));
+  CK(hipMemcpy(A, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(W, hW.data(), hW.size() * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(bias, hb.data(), N * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(R, hR.data(), hR.size() * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(ref_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, A, W, bias, R, ref, M, N, K, epi);
+  CK(hipDeviceSynchronize());
+
+  GemmArgs a{};
+  a.A = A; a.lda = K; a.W = W; a.C = C; a.ldc = nout; a.bias = bias; a.R = R; a.ldr = N; a.alpha = 1.f;
+  a.M = M; a.N = N; a.K = K; a.ws = ws; a.ws_cap = ws_cap; a.a_bf16 = 1; a.c_bf16 = cbf;
+  a.C2 = epi == 1 ? C2 : nullptr;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const double flop = 2.0 * M * N * (double)K;
+  char* list = strdup(argv[5]);
+  for (char* tok = strtok(list, ","); tok; tok = strtok(nullptr, ",")) {
+    const int vv = atoi(tok);
+    const int v = vv < 0 ? vv : (vv & 15);     // +16: N-partitioned XCD order, +32: non-temporal stores
+    a.order_n = vv >= 0 && (vv & 16);
+    a.nt_store = vv >= 0 && (vv & 32);
+    a.dbg = vv >= 0 ? (vv >> 6) & 7 : 0;      // +64 no epilogue, +128 no MFMA, +256 no K loop
+    // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
+    CK(hipMemset(C, 0, (size_t)M * nout * 4));
+    hipError_t rc = v < 0 ? gemm(a, epi, true, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0);
+    if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", v, hipGetErrorString(rc)); continue; }
+    CK(hipDeviceSynchronize());
+    CK(hipMemset(err, 0, 4));
+    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, cbf, ref, (int64_t)M * nout, err);
+    float herr;
+    CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 3; ++i) CK(v < 0 ? gemm(a, epi, true, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) CK(v < 0 ? gemm(a, epi, true, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0));
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / iters;
+    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g}\n",
+           M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr);
+    fflush(stdout);
+  }
+  return 0;
+}
