@@ -71,6 +71,13 @@ int tone_session_finalize(tone_session *s);
  * (batch, I/O pointers).  Default 0. */
 int tone_session_set_graph(tone_session *s, int enable);
 
+/* Optional per-frame decode outputs of later runs (device pointer, int32 [batch][10], or NULL):
+ *   frame_info = greedy CTC token (argmax over 35, first index on ties; tone/decoder.py:57)
+ *              | speech flag << 8 (exp(lp[33]) + exp(lp[34]) <= 0.9; tone/logprob_splitter.py:134)
+ * computed in the head kernel from the logprobs it writes.  Replaces the host-side argmax and
+ * threshold of GreedyCTCDecoder / StreamingLogprobSplitter (10 ids + 10 bits per stream-chunk). */
+int tone_session_set_frame_info(tone_session *s, int32_t *frame_info);
+
 /* One streaming step for `batch` independent streams.
  *   signal      int32  [batch][2400]          PCM, int16 range (validated by the caller)
  *   state_in    fp16   [batch][state_stride]  first 219729 elements are the flat state

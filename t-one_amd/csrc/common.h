@@ -48,6 +48,8 @@ constexpr int64_t kStateSize = 219729;
 constexpr float kRmsEps = 1e-8f;
 constexpr float kLnEps = 1e-5f;
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
 // Where stream b's state row lives: row b, or row slots[b] of a device-resident slab.
 struct StateRef {
   const __half* in;

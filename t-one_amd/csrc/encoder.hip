@@ -380,39 +380,76 @@ hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* sha
 
 // ---------------------------------------------------------------------------------------------
 // ConvASRDecoder.forward (conformer.py:338-354): 1x1 conv 384 -> 35 and log_softmax, fp32.
-// The 35 x 384 weight sits in LDS (rows padded to 385 floats: conflict-free per-lane rows);
-// one wave per frame, lane o < 35 owns logit o.
-__global__ void __launch_bounds__(256) head_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                   const float* __restrict__ bias, float* __restrict__ logp, int rows) {
-  __shared__ float ws[kVocab][kD + 1];
-  __shared__ float xs[4][kD];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int i = tid; i < kVocab * kD; i += 256) ws[i / kD][i % kD] = w[i];
+// One lane per frame row: the 35 vocabulary dot products accumulate in registers while x streams
+// through in 8-float slices and the (broadcast) weight rows come from LDS; log-softmax, the greedy
+// token and the splitter's speech flag are per-lane epilogues, and the wave's 64 x 35 logprob block
+// (contiguous in memory) leaves through LDS as coalesced stores.
+//   frame_info[row] = argmax_v logp[row][v] (first index on ties, decoder.py:57)
+//                   | (exp(logp[33]) + exp(logp[34]) <= 0.9) << 8      (logprob_splitter.py:134)
+constexpr float kSilenceThreshold = 0.9f;
+__global__ void __launch_bounds__(64) head_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                  const float* __restrict__ bias, float* __restrict__ logp,
+                                                  int32_t* __restrict__ frame_info, int rows) {
+  __shared__ __attribute__((aligned(16))) float ws[kVocab * kD];
+  __shared__ float lo[64 * kVocab];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < kVocab * kD / 4; i += 64)
+    reinterpret_cast<f32x4_t*>(ws)[i] = reinterpret_cast<const f32x4_t*>(w)[i];
   __syncthreads();
-  for (int base = blockIdx.x * 4; base < rows; base += gridDim.x * 4) {
-    const int row = base + wid;
-    const bool valid = row < rows;
-    __syncthreads();
-    if (valid)
-      for (int c = lane; c < kD; c += 64) xs[wid][c] = x[(int64_t)row * kD + c];
-    __syncthreads();
-    float z = -INFINITY;
-    if (lane < kVocab) {
-      float acc = 0.f;
-      for (int c = 0; c < kD; ++c) acc = fmaf(ws[lane][c], xs[wid][c], acc);
-      z = acc + bias[lane];
+  const int row0 = blockIdx.x * 64, row = row0 + lane;
+  const float* xr = x + (int64_t)min(row, rows - 1) * kD;
+  float acc[kVocab];
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) acc[v] = 0.f;
+  f32x4_t xa = reinterpret_cast<const f32x4_t*>(xr)[0], xb = reinterpret_cast<const f32x4_t*>(xr)[1];
+  for (int k = 0; k < kD; k += 8) {
+    const f32x4_t ca = xa, cb = xb;
+    if (k + 8 < kD) {
+      xa = reinterpret_cast<const f32x4_t*>(xr + k + 8)[0];
+      xb = reinterpret_cast<const f32x4_t*>(xr + k + 8)[1];
     }
-    const float m = wave_max(z);
-    const float e = lane < kVocab ? expf(z - m) : 0.f;
-    const float lse = logf(wave_sum(e));
-    if (valid && lane < kVocab) logp[(int64_t)row * kVocab + lane] = z - m - lse;
+#pragma unroll
+    for (int v = 0; v < kVocab; ++v) {
+      const f32x4_t wa = *reinterpret_cast<const f32x4_t*>(ws + v * kD + k);
+      const f32x4_t wb = *reinterpret_cast<const f32x4_t*>(ws + v * kD + k + 4);
+      float a = acc[v];
+      a = fmaf(wa.x, ca.x, a); a = fmaf(wa.y, ca.y, a); a = fmaf(wa.z, ca.z, a); a = fmaf(wa.w, ca.w, a);
+      a = fmaf(wb.x, cb.x, a); a = fmaf(wb.y, cb.y, a); a = fmaf(wb.z, cb.z, a); a = fmaf(wb.w, cb.w, a);
+      acc[v] = a;
+    }
   }
+  float m = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) {
+    acc[v] += bias[v];
+    m = fmaxf(m, acc[v]);
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) se += expf(acc[v] - m);
+  const float lse = logf(se);
+  float best = -INFINITY;
+  int tok = 0;
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) {
+    const float lp = acc[v] - m - lse;
+    lo[lane * kVocab + v] = lp;
+    if (lp > best) { best = lp; tok = v; }
+  }
+  if (frame_info && row < rows) {
+    const float sil = expf(lo[lane * kVocab + kVocab - 2]) + expf(lo[lane * kVocab + kVocab - 1]);
+    frame_info[row] = tok | ((sil <= kSilenceThreshold) ? 256 : 0);
+  }
+  __syncthreads();
+  const int nrow = min(64, rows - row0);
+  float* dst = logp + (int64_t)row0 * kVocab;
+  for (int i = lane; i < nrow * kVocab; i += 64) dst[i] = lo[i];
 }
 
-hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int rows, hipStream_t st) {
-  int blocks = (rows + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(head_kernel, dim3(blocks), dim3(256), 0, st, x, w, b, logp, rows);
+hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows,
+                       hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(head_kernel, dim3((rows + 63) / 64), dim3(64), 0, st, x, w, b, logp, frame_info, rows);
   return hipGetLastError();
 }
 

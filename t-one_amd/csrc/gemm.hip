@@ -52,6 +52,16 @@ __device__ __forceinline__ uint16_t bf16_bits(float a) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float sumsq_bf16x8(bf16x8 v, float acc) {
+  const bf16x2 p0 = __builtin_shufflevector(v, v, 0, 1), p1 = __builtin_shufflevector(v, v, 2, 3);
+  const bf16x2 p2 = __builtin_shufflevector(v, v, 4, 5), p3 = __builtin_shufflevector(v, v, 6, 7);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(p0, p0, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(p1, p1, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(p2, p2, acc, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(p3, p3, acc, false);
+}
+
 template <class T>
 __device__ __forceinline__ void st_out(T* ptr, T v, bool nt) {
   if (nt) __builtin_nontemporal_store(v, ptr);
@@ -162,6 +172,17 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[T
   }
 }
 
+// Workgroup barrier that leaves LDS-DMA (vmcnt) in flight: __syncthreads() fences with vmcnt(0).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // LDS-staged epilogue (LDS-DMA kernel): the wave tiles go to LDS as fp32 in the MFMA layout (the
 // stage buffers are free after the K loop), then the block writes whole output rows with 16-byte
 // fp32 / 8-byte bf16 vectors, so each 128-byte line leaves in one instruction instead of as 64-byte
@@ -178,17 +199,22 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
   float bcol[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) bcol[j] = (!SPLIT && p.bias) ? p.bias[n0 + wn * WTN + j * 32 + lr] : 0.f;
+  float inv[TM][16];                           // folded RMSNorm: 1 / (||a|| / sqrt(K) + eps) per row
+  const bool rs = !SPLIT && p.rowscale;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      inv[i][r] = rs ? 1.0f / rden[wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] : 1.0f;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int lrow = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      const float den = (!SPLIT && p.rowscale) ? rden[lrow] : 1.0f;
       if constexpr (PAIRED) {
 #pragma unroll
         for (int jp = 0; jp < TN / 2; ++jp) {
-          float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
-          if (p.rowscale) { g = g / den; u = u / den; }
+          float g = acc[i][2 * jp][r] * inv[i][r], u = acc[i][2 * jp + 1][r] * inv[i][r];
           g += bcol[2 * jp];
           u += bcol[2 * jp + 1];
           const float o = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);
@@ -198,16 +224,13 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           float v = acc[i][j][r];
-          if constexpr (!SPLIT) {
-            if (p.rowscale) v = v / den;
-            v += bcol[j];
-          }
+          if constexpr (!SPLIT) v = fmaf(v, inv[i][r], bcol[j]);
           Cs[lrow * BNO + wn * WTN + j * 32 + lr] = v;
         }
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   constexpr int RV = BNO / 4;                 // 4-float vectors per row
   constexpr int NV = TL::BM * RV / NT;        // vectors per thread
   static_assert(NV >= 1 && (TL::BM * RV) % NT == 0, "tile/thread mismatch");
@@ -223,11 +246,12 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
     }
   }
   const bool nt = p.nt_store;
+  const bool full = m0 + TL::BM <= p.M;        // block-uniform: no row guards
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int q = tid + k * NT, row = q / RV, c = (q % RV) * 4;
     const int grow = m0 + row;
-    if (grow >= p.M) continue;
+    if (!full && grow >= p.M) continue;
     f32x4 v = val[k];
     if constexpr (SPLIT) {
       st_out(reinterpret_cast<f32x4*>(p.ws + ((int64_t)blockIdx.y * p.M + grow) * p.N + n0 + c), v, nt);
@@ -268,8 +292,9 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
   constexpr int A_RV = BK / AVE;                         // vectors per A row per K-step
   static_assert(A_V >= 1 && W_V >= 1 && (NT % A_RV) == 0, "tile too small for the thread count");
 
-  __shared__ __attribute__((aligned(16))) ST As[2][BM * LDS_ROW];
-  __shared__ __attribute__((aligned(16))) ST Bs[2][BN * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) ST lds_all[2 * (BM + BN) * LDS_ROW];   // A and W stages; C tile after
+  ST(*As)[BM * LDS_ROW] = reinterpret_cast<ST(*)[BM * LDS_ROW]>(lds_all);
+  ST(*Bs)[BN * LDS_ROW] = reinterpret_cast<ST(*)[BN * LDS_ROW]>(lds_all + 2 * BM * LDS_ROW);
   __shared__ float rden[BM];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -444,7 +469,13 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
     }
   }
 
-  gemm_epilogue<TL, EPI, CBF, SPLIT>(p, acc, rden, m0, n0, wm, wn, lane);
+  constexpr bool kLdsEpi = (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU || EPI == EPI_GLU) &&
+                           BM * BN * 4 <= (int)sizeof(lds_all);
+  if constexpr (kLdsEpi) {
+    gemm_epilogue_lds<TL, EPI, CBF, SPLIT>(p, acc, rden, reinterpret_cast<float*>(lds_all), m0, n0, wm, wn, tid);
+  } else {
+    gemm_epilogue<TL, EPI, CBF, SPLIT>(p, acc, rden, m0, n0, wm, wn, lane);
+  }
 }
 
 
@@ -457,10 +488,6 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
 // A rowscale GEMM reads the bf16 shadow of the residual and takes each row's sum of squares from
 // its own A fragments (waves of the first N column only).
 // Split-K is a runtime mode here (p.k_split > 0: K slice blockIdx.y, raw partials to p.ws).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 template <class TL, int EPI, bool CBF, int S>
 __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArgs p) {
@@ -472,6 +499,7 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
   constexpr bool CONV2 = (EPI == EPI_CONV2);
   constexpr int A_I = BM / 8 / kNWaves, W_I = BN / 8 / kNWaves;     // DMA wave-instructions per K-step
   static_assert(A_I >= 1 && W_I >= 1 && BM % (8 * kNWaves) == 0 && BN % (8 * kNWaves) == 0, "tile/wave mismatch");
+  static_assert(!(EPI == EPI_SWIGLU || EPI == EPI_GLU) || TN % 2 == 0, "paired epilogues pair n-tiles");
   constexpr int kStageElems = (BM + BN) * BK;                    // bf16 elements per buffer
   static_assert(S >= 2 && S <= 4, "2..4 LDS stages");
   constexpr int kIps = A_I + W_I;                                // DMA instructions per stage per thread
@@ -567,38 +595,32 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
   const int lr = lane & 31, lh = lane >> 5;
   auto compute = [&](int buf) {
     const uint16_t* base = lds + buf * kStageElems;
+    // all fragments of the K-step first (one counted LDS wait), then the MFMAs
+    bf16x8 a[BK / 16][TM], b[BK / 16][TN];
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       const int slot = ks * 2 + lh;
-      bf16x8 a[TM], b[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WTM + i * 32 + lr;
-        a[i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((slot ^ (row & 7)) << 3));
+        a[ks][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((slot ^ (row & 7)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WTN + j * 32 + lr;
-        b[j] = *reinterpret_cast<const bf16x8*>(base + (BM + row) * BK + ((slot ^ (row & 7)) << 3));
+        b[ks][j] = *reinterpret_cast<const bf16x8*>(base + (BM + row) * BK + ((slot ^ (row & 7)) << 3));
       }
-      if (want_ss) {
+    }
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = (float)a[i][e];
-            ss[i] = fmaf(v, v, ss[i]);
-          }
-      }
-      if (p.dbg & 2) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) acc[i][0][0] += (float)a[i][0] + (float)b[0][i & 1];
-        continue;
-      }
+    for (int ks = 0; ks < BK / 16; ++ks) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
+      // row sums of squares for a folded RMSNorm (v_dot2 on bf16 pairs, beside the MFMAs)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) ss[i] = sumsq_bf16x8(a[ks][i], ss[i]);
     }
   };
 
@@ -612,7 +634,7 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
     if (S >= 4 && ahead >= 2) wait_vmcnt<(S >= 4 ? 2 * kIps : 0)>();
     else if (S >= 3 && ahead >= 1) wait_vmcnt<(S >= 3 ? kIps : 0)>();
     else wait_vmcnt<0>();
-    __syncthreads();
+    lds_barrier();   // not __syncthreads(): its vmcnt(0) fence would drain the DMAs kept in flight
     if (kt + S - 1 < nk) stage((kt + S - 1) % S, kb + (kt + S - 1) * BK);
     compute(kt % S);
   }
@@ -659,6 +681,143 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
     }
   }
   gemm_epilogue<TL, EPI, CBF, false>(p, acc, rden, m0, n0, wm, wn, lane);
+}
+
+// Persistent bf16 GEMM (large M): one workgroup per CU walks its tiles with ONE LDS-DMA ring that
+// runs across tile boundaries, so the first K-steps of tile i+1 are in flight while tile i's
+// epilogue (LDS-staged, its own LDS region) drains -- no per-tile prologue bubble and no idle
+// memory pipe during stores.  Tiles are dealt XCD-contiguously: the workgroups of one XCD walk
+// neighbouring tiles together, so an A row-block is fetched into that XCD's L2 once.
+// Plain row-major A only (no rpg / conv2 gathers), no split-K.
+template <class TL, int EPI, bool CBF>
+__global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_persist_kernel(GemmArgs p) {
+  constexpr int BM = TL::BM, BN = TL::BN, WM = TL::WM, WN = TL::WN;
+  constexpr int kNWaves = WM * WN, NT = kNWaves * 64;
+  constexpr int BK = 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_I = BM / 8 / kNWaves, W_I = BN / 8 / kNWaves;
+  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
+  constexpr int BNO = PAIRED ? BN / 2 : BN;
+  static_assert(A_I >= 1 && W_I >= 1, "tile/wave mismatch");
+  static_assert(EPI == EPI_STORE || EPI == EPI_RESID || PAIRED, "persistent GEMM: STORE/RESID/SWIGLU/GLU");
+  constexpr int kStageElems = (BM + BN) * BK;
+  // ONE LDS object (a second __shared__ array can make hipcc fence every ds_read behind the DMAs)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kStageElems + 2 * BM * BNO + 2 * BM];
+  float* Cs = reinterpret_cast<float*>(lds + 2 * kStageElems);
+  float* rden = Cs + BM * BNO;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = p.N / BN, ntm = (p.M + BM - 1) / BM, ntiles = ntm * ntn;
+  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int q = (ntiles + 7) >> 3, tbeg = xcd * q, tend = min(ntiles, tbeg + q);
+  const int ntile_mine = (tend - tbeg - jb + nxb - 1) / nxb;    // tiles tbeg+jb, +nxb, ...
+  if (ntile_mine <= 0) return;
+  const int nk = p.K / BK;
+  const int G = ntile_mine * nk;                                 // K-steps of all my tiles
+  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
+  const uint16_t* __restrict__ W = static_cast<const uint16_t*>(p.W);
+  const int lrow8 = lane >> 3, lslot = lane & 7;
+
+  auto tile_mn = [&](int g, int& m0, int& n0) {
+    const int t = tbeg + jb + (g / nk) * nxb;
+    m0 = (t / ntn) * BM;
+    n0 = (t % ntn) * BN;
+  };
+  auto stage = [&](int buf, int g) {
+    int m0, n0;
+    tile_mn(g, m0, n0);
+    const int k0 = (g % nk) * BK;
+    uint16_t* base = lds + buf * kStageElems;
+    (void)base;
+#pragma unroll
+    for (int i = 0; i < A_I; ++i) {
+      const int row = 8 * (wid + i * kNWaves) + lrow8;
+      const int gm = min(m0 + row, p.M - 1);
+      const uint16_t* src = A + (int64_t)gm * p.lda + k0 + ((lslot ^ (row & 7)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + (8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < W_I; ++i) {
+      const int row = 8 * (wid + i * kNWaves) + lrow8;
+      const uint16_t* src = W + (int64_t)(n0 + row) * p.K + k0 + ((lslot ^ (row & 7)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + (BM + 8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+
+  f32x16 acc[TM][TN];
+  float ss[TM];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      ss[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
+  };
+  zero();
+  const bool want_ss = p.rowscale && wn == 0;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  stage(0, 0);
+  for (int g = 0; g < G; ++g) {
+    wait_vmcnt<0>();
+    lds_barrier();
+    if (g + 1 < G) stage((g + 1) & 1, g + 1);
+    const uint16_t* base = lds + (g & 1) * kStageElems;
+    bf16x8 a[BK / 16][TM], b[BK / 16][TN];
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int slot = ks * 2 + lh;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 32 + lr;
+        a[ks][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((slot ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WTN + j * 32 + lr;
+        b[ks][j] = *reinterpret_cast<const bf16x8*>(base + (BM + row) * BK + ((slot ^ (row & 7)) << 3));
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) ss[i] = sumsq_bf16x8(a[ks][i], ss[i]);
+    }
+    if (g % nk == nk - 1) {   // tile finished: epilogue while the next tile's first K-step loads
+      int m0, n0;
+      tile_mn(g, m0, n0);
+      if (p.rowscale) {
+        if (want_ss) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const float v = ss[i] + __shfl_xor(ss[i], 32, 64);
+            if (lh == 0) rden[wm * WTM + i * 32 + lr] = sqrtf(v) * p.inv_sqrt_k + kRmsEps;
+          }
+        }
+        lds_barrier();
+      }
+      gemm_epilogue_lds<TL, EPI, CBF, false>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
+      zero();
+    }
+  }
 }
 
 // Split-K combine: fixed-order sum of the partials, then the STORE/RESID epilogue.
@@ -775,7 +934,8 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   constexpr int kTarget = 512;
   const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);
   const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
-  if (t128 >= kTarget) return launch_glds_epi<Tile<128, 128, 2, 2>>(a, epi, 1, st);
+  // 8 waves of 32x64 per 128x128 tile once there is a tile per CU (tools/gemm_bench sweep)
+  if (t128 >= kTarget / 2) return launch_glds_epi<Tile<128, 128, 4, 2>>(a, epi, 1, st);
   int nsplit = 1;
   if ((epi == EPI_STORE || epi == EPI_RESID) && a.ws && t64 < kTarget) {
     const int ksteps = a.K / 64;
@@ -788,6 +948,39 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   }
   if (nsplit > 1 || t64 >= kTarget / 2) return launch_glds_epi<Tile<64, 128, 2, 2>>(a, epi, nsplit, st);
   return launch_glds_epi<Tile<32, 128, 1, 2>>(a, epi, 1, st);
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <class TL, int EPI, bool CBF>
+static hipError_t launch_persist(const GemmArgs& a, int per_cu, hipStream_t st) {
+  if (a.N % TL::BN || a.K % 64 || a.rpg) return hipErrorInvalidValue;
+  const int tiles = ((a.M + TL::BM - 1) / TL::BM) * (a.N / TL::BN);
+  int grid = num_cus() * per_cu;
+  const int need = ((tiles + 7) / 8) * 8;
+  if (grid > need) grid = need;
+  grid = (grid + 7) / 8 * 8;
+  hipLaunchKernelGGL((gemm_persist_kernel<TL, EPI, CBF>), dim3(grid), dim3(TL::WM * TL::WN * 64), 0, st, a);
+  return hipGetLastError();
+}
+
+template <class TL>
+static hipError_t launch_persist_epi(const GemmArgs& a, int epi, int per_cu, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return a.c_bf16 ? launch_persist<TL, EPI_STORE, true>(a, per_cu, st) : launch_persist<TL, EPI_STORE, false>(a, per_cu, st);
+    case EPI_RESID: return launch_persist<TL, EPI_RESID, false>(a, per_cu, st);
+    case EPI_SWIGLU: return a.c_bf16 ? launch_persist<TL, EPI_SWIGLU, true>(a, per_cu, st) : launch_persist<TL, EPI_SWIGLU, false>(a, per_cu, st);
+    case EPI_GLU: return a.c_bf16 ? launch_persist<TL, EPI_GLU, true>(a, per_cu, st) : launch_persist<TL, EPI_GLU, false>(a, per_cu, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 // Fixed bf16 tile/stage variants (tools/gemm_bench.hip), bypassing the size heuristics.
@@ -803,6 +996,11 @@ hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit
     case 7: return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, nsplit, st);
     case 8: return launch_glds_epi<Tile<64, 128, 2, 2>, 3>(a, epi, nsplit, st);
     case 9: return launch_glds_epi<Tile<64, 128, 2, 2>, 4>(a, epi, nsplit, st);
+    case 10: return launch_persist_epi<Tile<128, 128, 2, 2>>(a, epi, 1, st);
+    case 11: return launch_persist_epi<Tile<64, 128, 2, 2>>(a, epi, 1, st);
+    case 12: return launch_persist_epi<Tile<64, 128, 2, 2>>(a, epi, 2, st);
+    case 13: return launch_persist_epi<Tile<128, 128, 2, 2>>(a, epi, 2, st);
+    case 14: return launch_glds_epi<Tile<128, 128, 4, 2>, 2>(a, epi, nsplit, st);
     default: return hipErrorInvalidValue;
   }
 }

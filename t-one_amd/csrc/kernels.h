@@ -37,7 +37,7 @@ struct GemmArgs {
   uint16_t* C2;       // STORE/RESID: optional bf16 shadow of C (same ldc), feeds bf16 GEMMs
   int order_n;        // bf16 LDS-DMA kernel: XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8) (large W)
   int nt_store;       // non-temporal epilogue stores
-  int dbg;            // microbenchmark only: 1 = no epilogue, 2 = no MFMA, 4 = no K loop
+  int dbg;            // microbenchmark only: 1 = no epilogue, 4 = no K loop
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -101,6 +101,8 @@ hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const 
 hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, hipStream_t st);
 
 // a14: logits = x . Wd^T + bd, log_softmax over 35 classes -> logprobs [B*10][35]
-hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int rows, hipStream_t st);
+// a14 + decode flags: logprobs [rows][35]; optional frame_info[row] = greedy token | speech flag << 8
+hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows,
+                       hipStream_t st);
 
 }  // namespace tone

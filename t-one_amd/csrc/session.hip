@@ -72,6 +72,7 @@ struct tone_session {
   int max_batch = 0;
   bool finalized = false;
   bool use_graph = false;
+  int32_t* frame_info = nullptr;   // optional [batch*10] greedy token | speech flag << 8
   bool timing = false;
   int debug_stop = -1;
   std::map<std::string, std::vector<float>> host;
@@ -98,7 +99,7 @@ struct tone_session {
   // graphs
   struct GraphKey {
     int batch;
-    const void *a, *b, *c, *d, *e;
+    const void *a, *b, *c, *d, *e, *f;
     int64_t stride;
     bool operator<(const GraphKey& o) const {
       return std::memcmp(this, &o, sizeof(GraphKey)) < 0;
@@ -410,7 +411,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     }
     if (s->debug_stop == 2 + l) return TONE_OK;
   }
-  LAUNCH("head", launch_head(s->rA, s->whead, s->bhead, logp, B * kT, st));
+  LAUNCH("head", launch_head(s->rA, s->whead, s->bhead, logp, s->frame_info, B * kT, st));
   return TONE_OK;
 }
 
@@ -677,6 +678,7 @@ int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp,
     k.c = sr.out;
     k.d = logp;
     k.e = sr.slots;
+    k.f = s->frame_info;
     k.stride = sr.stride;
     (void)key_a;
     (void)key_b;
@@ -761,6 +763,12 @@ int tone_session_finalize(tone_session* s) {
 int tone_session_set_graph(tone_session* s, int enable) {
   if (!s) return fail(TONE_E_INVALID, "null session");
   s->use_graph = enable != 0;
+  return TONE_OK;
+}
+
+int tone_session_set_frame_info(tone_session* s, int32_t* frame_info) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  s->frame_info = frame_info;
   return TONE_OK;
 }
 

@@ -80,6 +80,16 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ref, (size_t)M * nout * 4)); CK(hipMalloc(&err, 4));
   const int64_t ws_cap = (int64_t)16 * M * N;
   CK(hipMalloc(&ws, ws_cap * 4));
+  // fp32 copies of the same (bf16-representable) operands for the fp32 path (variant -2)
+  float *Af, *Wf;
+  {
+    std::vector<float> fa(hA.size()), fw(hW.size());
+    for (size_t i = 0; i < hA.size(); ++i) { uint32_t u = (uint32_t)hA[i] << 16; memcpy(&fa[i], &u, 4); }
+    for (size_t i = 0; i < hW.size(); ++i) { uint32_t u = (uint32_t)hW[i] << 16; memcpy(&fw[i], &u, 4); }
+    CK(hipMalloc(&Af, fa.size() * 4)); CK(hipMalloc(&Wf, fw.size() * 4));
+    CK(hipMemcpy(Af, fa.data(), fa.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(Wf, fw.data(), fw.size() * 4, hipMemcpyHostToDevice));
+  }
   CK(hipMemcpy(A, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(W, hW.data(), hW.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(bias, hb.data(), N * 4, hipMemcpyHostToDevice));
@@ -103,16 +113,22 @@ int main(int argc, char** argv) {
     a.dbg = vv >= 0 ? (vv >> 6) & 7 : 0;      // +64 no epilogue, +128 no MFMA, +256 no K loop
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
-    hipError_t rc = v < 0 ? gemm(a, epi, true, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0);
+    const bool f32 = (vv == -2);
+    a.A = f32 ? (const void*)Af : (const void*)A;
+    a.W = f32 ? (const void*)Wf : (const void*)W;
+    a.a_bf16 = !f32;
+    a.c_bf16 = f32 ? 0 : cbf;
+    auto launch = [&]() { return v < 0 ? gemm(a, epi, !f32, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0); };
+    hipError_t rc = launch();
     if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", v, hipGetErrorString(rc)); continue; }
     CK(hipDeviceSynchronize());
     CK(hipMemset(err, 0, 4));
-    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, cbf, ref, (int64_t)M * nout, err);
+    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, a.c_bf16, ref, (int64_t)M * nout, err);
     float herr;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
-    for (int i = 0; i < 3; ++i) CK(v < 0 ? gemm(a, epi, true, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0));
+    for (int i = 0; i < 3; ++i) CK(launch());
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < iters; ++i) CK(v < 0 ? gemm(a, epi, true, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0));
+    for (int i = 0; i < iters; ++i) CK(launch());
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms;

@@ -86,6 +86,20 @@ class ToneSession:
                                                     int(signal.shape[0]), st),
                    "tone_session_run_slots")
 
+    def set_frame_info(self, frame_info=None) -> None:
+        """Have later runs also write frame_info int32 (>= max_batch, 10): greedy token | speech << 8
+        (include/tonehip.h); None switches it off."""
+        torch = _torch()
+        ptr = 0
+        if frame_info is not None:
+            if frame_info.dtype != torch.int32 or frame_info.device != self.dev or not frame_info.is_contiguous():
+                raise ValueError(f"frame_info must be a contiguous int32 tensor on {self.dev}")
+            if frame_info.numel() < self.max_batch * C.CHUNK_FRAMES:
+                raise ValueError(f"frame_info needs >= {self.max_batch * C.CHUNK_FRAMES} elements")
+            ptr = frame_info.data_ptr()
+        self._frame_info = frame_info
+        _lib.check(self._lib.tone_session_set_frame_info(self._h, ptr), "tone_session_set_frame_info")
+
     def step(self, signal, state=None):
         """Allocate-and-run convenience: returns (logprobs, next_state) device tensors."""
         torch = _torch()

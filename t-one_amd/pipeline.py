@@ -1,0 +1,215 @@
+"""Batched streaming recognition on the device frame info.
+
+The reference pipeline (tone/pipeline.py:141-176) moves a (10, 35) fp32 logprob block per stream and
+chunk to the host, where ``StreamingLogprobSplitter`` thresholds exp(lp[33]) + exp(lp[34]) and
+``GreedyCTCDecoder`` takes the argmax.  Here the head kernel already emits both per frame
+(``frame_info`` = token | speech << 8, include/tonehip.h), so one step returns 10 int32 per stream
+and the splitter / greedy decoder below run on (token, speech) frames with the reference's rules:
+
+  * phrase boundaries       logprob_splitter.py:61-88   silences >= 20 frames separate phrases,
+                                                       speech longer than 2000 frames is force-split,
+                                                       only finished phrases are emitted
+  * phrase extent           logprob_splitter.py:136-156 +-3 frames around the phrase, buffer kept
+                                                       from the last phrase end (or last 3 frames)
+  * greedy text             decoder.py:57-59            collapse repeats, drop blank (34), strip
+  * phrase times            pipeline.py:151-168
+
+``StreamingGreedyPipeline`` serves many concurrent streams from one ``ToneSession``: each stream owns
+a row ("slot") of a device-resident state slab, every step runs the active streams as one batch
+through ``tone_session_run_slots``, and only the frame info crosses PCIe.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import config as C
+
+LABELS = "абвгдеёжзийклмнопрстуфхцчшщъыьэюя "   # tone/decoder.py:24; token 34 = blank
+MIN_SILENCE = 20        # logprob_splitter.py:58
+SPEECH_EXPAND = 3       # logprob_splitter.py:59
+MAX_PHRASE = 2000       # logprob_splitter.py:60
+PADDING = 2400          # pipeline.py:40 (300 ms of left/right padding used by forward_offline)
+STATE_STRIDE = 219776   # slab row stride: 219729 rounded up to 64 elements (128-byte aligned rows)
+
+
+@dataclass
+class TextPhrase:
+    """tone/pipeline.py:16-27."""
+    text: str
+    start_time: float
+    end_time: float
+
+
+@dataclass
+class FrameSplitterState:
+    """Frames carried between steps (the reference keeps the logprob rows, logprob_splitter.py:36-40)."""
+    tokens: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    speech: np.ndarray = field(default_factory=lambda: np.zeros(0, bool))
+    offset: int = 0
+
+
+def decode_frame_info(info: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    info = np.asarray(info, np.int32)
+    return (info & 0xFF).astype(np.int32), (info >> 8).astype(bool)
+
+
+def greedy_text(tokens: np.ndarray) -> str:
+    toks = np.asarray(tokens)
+    if toks.size == 0:
+        return ""
+    keep = np.ones(toks.size, bool)
+    keep[1:] = toks[1:] != toks[:-1]
+    toks = toks[keep]
+    return "".join(LABELS[t] for t in toks.tolist() if t < len(LABELS)).strip()
+
+
+def _phrases(speech: np.ndarray, is_last: bool) -> list[tuple[int, int]]:
+    n = speech.size
+    silent = np.concatenate([np.ones(MIN_SILENCE, bool), ~speech, np.ones(MIN_SILENCE if is_last else 0, bool)])
+    edges = np.diff(np.concatenate([[0], silent.astype(np.int8), [0]]))
+    starts = np.flatnonzero(edges == 1) - MIN_SILENCE
+    ends = np.flatnonzero(edges == -1) - MIN_SILENCE
+    sep = (ends - starts) >= MIN_SILENCE
+    starts, ends = starts[sep].tolist(), ends[sep].tolist()
+    out = []
+    for k, beg in enumerate(ends):
+        stop = starts[k + 1] if k + 1 < len(starts) else n
+        while stop - beg >= MAX_PHRASE:
+            out.append((beg, beg + MAX_PHRASE))
+            beg += MAX_PHRASE
+        if k + 1 < len(starts):
+            out.append((beg, stop))
+    return out
+
+
+def split_frames(tokens: np.ndarray, speech: np.ndarray, state: Optional[FrameSplitterState], *,
+                 is_last: bool = False) -> tuple[list[tuple[np.ndarray, int, int]], FrameSplitterState]:
+    """One splitter step on frames -> ([(phrase tokens, start_frame, end_frame)], next state)."""
+    state = state or FrameSplitterState()
+    toks = np.concatenate([state.tokens, np.asarray(tokens, np.int32)])
+    sp = np.concatenate([state.speech, np.asarray(speech, bool)])
+    out, last = [], 0
+    for s, e in _phrases(sp, is_last):
+        out.append((toks[max(0, s - SPEECH_EXPAND):e + SPEECH_EXPAND], s + state.offset, e + state.offset))
+        last = e
+    if not sp[last:].any():
+        last = max(last, sp.size - SPEECH_EXPAND)
+    return out, FrameSplitterState(toks[last:], sp[last:], state.offset + last)
+
+
+def phrase_times(start_frame: int, end_frame: int) -> tuple[float, float]:
+    shift = C.MEAN_TIME_BIAS + PADDING / C.SAMPLE_RATE
+    st = max(0, round(start_frame * C.FRAME_SIZE - shift, 2))
+    return st, max(st, round(end_frame * C.FRAME_SIZE - shift, 2))
+
+
+def frames_to_phrases(tokens, speech, state, *, is_last=False) -> tuple[list[TextPhrase], FrameSplitterState]:
+    found, state = split_frames(tokens, speech, state, is_last=is_last)
+    return [TextPhrase(greedy_text(t), *phrase_times(s, e)) for t, s, e in found], state
+
+
+class StreamingGreedyPipeline:
+    """Many concurrent streams, one device batch per step, greedy CTC decoding on device frame info.
+
+    Drop-in counterpart of ``StreamingCTCPipeline(model, StreamingLogprobSplitter(), GreedyCTCDecoder())``
+    (tone/pipeline.py) for a server: ``open_stream`` / ``close_stream`` manage slots of the device
+    state slab, ``forward`` advances any subset of open streams by one 300 ms chunk each.
+    """
+
+    CHUNK_SIZE = C.AUDIO_CHUNK_SAMPLES
+
+    def __init__(self, session, n_slots: int):
+        import torch
+        if n_slots <= 0:
+            raise ValueError("n_slots must be positive")
+        self.session = session
+        self.n_slots = int(n_slots)
+        dev = session.dev
+        # two slabs: a step reads slab[cur] and writes slab[1 - cur] (run_slots must not alias)
+        self._slab = [torch.zeros((self.n_slots, STATE_STRIDE), dtype=torch.float16, device=dev) for _ in range(2)]
+        self._cur = 0
+        self._open: dict[int, FrameSplitterState] = {}
+        self._free = list(range(self.n_slots - 1, -1, -1))
+        mb = session.max_batch
+        self._info = torch.zeros((mb, C.CHUNK_FRAMES), dtype=torch.int32, device=dev)
+        self._logp = torch.empty((mb, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev)
+        session.set_frame_info(self._info)
+
+    # --- slots -------------------------------------------------------------------------------
+    def open_stream(self) -> int:
+        if not self._free:
+            raise RuntimeError(f"all {self.n_slots} stream slots are in use")
+        slot = self._free.pop()
+        self._slab[self._cur][slot].zero_()          # onnx_wrapper.py:114-115: zero state at stream start
+        self._open[slot] = FrameSplitterState()
+        return slot
+
+    def close_stream(self, slot: int) -> None:
+        if slot not in self._open:
+            raise KeyError(f"slot {slot} is not open")
+        del self._open[slot]
+        self._free.append(slot)
+
+    @property
+    def open_slots(self) -> list[int]:
+        return sorted(self._open)
+
+    # --- one step ----------------------------------------------------------------------------
+    def forward(self, chunks: np.ndarray, slots: Sequence[int], is_last: Optional[Sequence[bool]] = None
+                ) -> list[list[TextPhrase]]:
+        """chunks int32 (n, 2400) for the open streams ``slots`` -> per stream, the finished phrases."""
+        import torch
+        if not isinstance(chunks, np.ndarray):
+            raise TypeError(f"Incorrect 'chunks' type: expected np.ndarray, but got {type(chunks)}")
+        n = len(slots)
+        if chunks.shape != (n, self.CHUNK_SIZE):
+            raise ValueError(f"Shape of 'chunks' must be ({n}, {self.CHUNK_SIZE}), but got {chunks.shape}")
+        if chunks.dtype != np.int32:
+            raise ValueError(f"Incorrect dtype of 'chunks': expected np.int32, but got {chunks.dtype}")
+        if n and (chunks.min() < -32768 or chunks.max() > 32767):
+            raise ValueError("Audio samples must be in the int16 range [-32768, 32767]")
+        if len(set(slots)) != n or any(s not in self._open for s in slots):
+            raise ValueError("slots must be distinct open stream slots")
+        is_last = [False] * n if is_last is None else list(is_last)
+        src, dst = self._slab[self._cur], self._slab[1 - self._cur]
+        idle = [s for s in self._open if s not in set(slots)]
+        if idle:   # streams without a chunk this step keep their state: carry their rows across
+            idx = torch.tensor(idle, dtype=torch.int64, device=src.device)
+            dst.index_copy_(0, idx, src.index_select(0, idx))
+        out: list[list[TextPhrase]] = []
+        mb = self.session.max_batch
+        info = np.empty((n, C.CHUNK_FRAMES), np.int32)
+        for b0 in range(0, n, mb):
+            b1 = min(n, b0 + mb)
+            sig = torch.from_numpy(np.ascontiguousarray(chunks[b0:b1])).to(src.device)
+            sl = torch.tensor(list(slots[b0:b1]), dtype=torch.int32, device=src.device)
+            self.session.run_slots(sig, sl, src, dst, self._logp[:b1 - b0])
+            info[b0:b1] = self._info[:b1 - b0].cpu().numpy()
+        self._cur ^= 1
+        for i, slot in enumerate(slots):
+            toks, speech = decode_frame_info(info[i])
+            phrases, self._open[slot] = frames_to_phrases(toks, speech, self._open[slot], is_last=is_last[i])
+            out.append(phrases)
+        return out
+
+    def forward_offline(self, audio: np.ndarray) -> list[TextPhrase]:
+        """tone/pipeline.py:178-200 on one stream: pad 300 ms both sides, pad to whole chunks, decode."""
+        if not isinstance(audio, np.ndarray):
+            raise TypeError(f"Incorrect 'audio' type: expected np.ndarray, but got {type(audio)}")
+        if audio.ndim != 1:
+            raise ValueError(f"Shape of 'audio' must be (L,), but got {audio.shape}")
+        audio = np.pad(audio.astype(np.int32), (PADDING, PADDING))
+        audio = np.pad(audio, (0, -len(audio) % self.CHUNK_SIZE))
+        chunks = audio.reshape(-1, self.CHUNK_SIZE)
+        slot = self.open_stream()
+        try:
+            phrases: list[TextPhrase] = []
+            for i, ch in enumerate(chunks):
+                phrases += self.forward(ch[None], [slot], [i == len(chunks) - 1])[0]
+            return phrases
+        finally:
+            self.close_stream(slot)

@@ -1,0 +1,195 @@
+"""Decode side: device frame info, frame-based splitter + greedy decoder,
+multi-stream slot pipeline.
+
+CPU: the oracle restatement (oracle/tone_decode_oracle.py) against the reference splitter's own
+outputs (tests/golden/golden_decode.npz, made by tests/golden/make_golden_decode.py), and the
+product's frame-based splitter (tone_amd.pipeline) against the same fixture.
+GPU: frame_info from the head kernel against argmax / threshold of the logprobs it wrote, and the
+slot pipeline (idle streams, late joins) against per-stream sequential runs.
+"""
+
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import tone_decode_oracle as O
+from tone_amd import pipeline as P
+
+GOLD = Path(__file__).parent / "golden" / "golden_decode.npz"
+
+
+def _golden():
+    g = np.load(GOLD)
+    phrases = json.loads(bytes(g["phrases"]).decode())
+    offs = np.concatenate([[0], np.cumsum(g["lengths"])])
+    streams = [g["logprobs"][offs[i]:offs[i + 1]] for i in range(len(g["lengths"]))]
+    return streams, phrases
+
+
+def test_oracle_matches_reference_splitter_and_decoder():
+    streams, want = _golden()
+    got = []
+    for si, lp in enumerate(streams):
+        st, n = None, len(lp) // 10
+        for c in range(n):
+            out, st = O.splitter_step(lp[10 * c:10 * c + 10], st, c == n - 1)
+            for plp, s, e in out:
+                t0, t1 = O.phrase_times(s, e)
+                got.append({"stream": si, "chunk": c, "text": O.greedy_text(plp), "start_frame": s, "end_frame": e,
+                            "start_time": t0, "end_time": t1, "n_logprob_rows": len(plp)})
+    assert len(want) >= 40
+    assert got == want
+
+
+def test_frame_splitter_matches_reference():
+    """tone_amd.pipeline on (argmax, speech) frames == the reference splitter + greedy decoder on logprobs."""
+    streams, want = _golden()
+    got = []
+    for si, lp in enumerate(streams):
+        st, n = None, len(lp) // 10
+        toks = np.argmax(lp, axis=-1).astype(np.int32)
+        speech = np.exp(lp[:, -2:]).sum(axis=-1) <= 0.9
+        info = toks | (speech.astype(np.int32) << 8)
+        for c in range(n):
+            t, sp = P.decode_frame_info(info[10 * c:10 * c + 10])
+            found, st = P.split_frames(t, sp, st, is_last=c == n - 1)
+            for ptok, s, e in found:
+                t0, t1 = P.phrase_times(s, e)
+                got.append({"stream": si, "chunk": c, "text": P.greedy_text(ptok), "start_frame": s, "end_frame": e,
+                            "start_time": t0, "end_time": t1, "n_logprob_rows": len(ptok)})
+    assert got == want
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_frame_splitter_random_vs_oracle(seed):
+    """Random speech/silence masks (short silences, 19/20/21-frame edges, > 2000-frame speech)."""
+    rng = np.random.default_rng(seed)
+    n = 4200 + 10 * int(rng.integers(0, 50))
+    speech = np.zeros(n, bool)
+    t = 0
+    while t < n:
+        run = int(rng.choice([rng.integers(1, 25), rng.integers(2000, 2300)], p=[0.9, 0.1]))
+        speech[t:t + run] = bool(rng.integers(2))
+        t += run
+    toks = rng.integers(0, 35, n).astype(np.int32)
+    # logprobs consistent with (toks, speech) for the oracle: blank/space mass decides speech
+    lp = np.full((n, 35), -30.0, np.float32)
+    lp[np.arange(n), toks] = -0.01
+    lp[:, 34] = np.where(speech, -30.0, -0.01)
+    lp[~speech & (toks != 34), toks[~speech & (toks != 34)]] = -5.0
+    speech = np.exp(lp[:, -2:]).sum(-1) <= np.float32(0.9)     # the head kernel's flag rule
+    st_o, st_p = None, None
+    for c in range(n // 10):
+        last = c == n // 10 - 1
+        o, st_o = O.splitter_step(lp[10 * c:10 * c + 10], st_o, last)
+        p, st_p = P.split_frames(np.argmax(lp[10 * c:10 * c + 10], -1), speech[10 * c:10 * c + 10], st_p, is_last=last)
+        assert [(s, e) for _, s, e in o] == [(s, e) for _, s, e in p]
+        assert [O.greedy_text(a) for a, _, _ in o] == [P.greedy_text(a) for a, _, _ in p]
+        assert st_o.offset == st_p.offset and len(st_o.past) == len(st_p.tokens)
+
+
+def test_greedy_text_rules():
+    assert P.greedy_text(np.array([34, 0, 0, 34, 0, 33, 33, 1, 34])) == "аа б"
+    assert P.greedy_text(np.array([], np.int32)) == ""
+    assert P.greedy_text(np.array([33, 33, 34])) == ""
+
+
+# --------------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def session():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from tone_amd.model import ToneSession
+    from tone_amd.weights import synthetic_weights
+    return ToneSession(synthetic_weights(0), device=0, precision="fp32", max_batch=8)
+
+
+def _pcm(rng, b):
+    x = np.clip(rng.normal(0, 3000, (b, 2400)), -32768, 32767).astype(np.int32)
+    x[rng.random(b) < 0.2] = 0
+    return x
+
+
+@pytest.mark.gpu
+def test_frame_info_matches_logprobs(session):
+    import torch
+    rng = np.random.default_rng(5)
+    info = torch.full((8, 10), -1, dtype=torch.int32, device=session.dev)
+    session.set_frame_info(info)
+    try:
+        state = None
+        for _ in range(3):
+            sig = torch.from_numpy(_pcm(rng, 8)).to(session.dev)
+            logp, state = session.step(sig, state)
+            lp = logp.cpu().numpy()
+            got = info.cpu().numpy()
+            assert np.array_equal(got & 0xFF, np.argmax(lp, -1))
+            ssum = np.exp(lp[..., -2:]).sum(-1)
+            flag = (got >> 8).astype(bool)
+            mism = flag != (ssum <= np.float32(0.9))
+            assert not np.any(mism & (np.abs(ssum - 0.9) > 1e-6))
+    finally:
+        session.set_frame_info(None)
+
+
+@pytest.mark.gpu
+def test_slot_pipeline_matches_sequential_streams(session):
+    import torch
+    rng = np.random.default_rng(11)
+    pipe = P.StreamingGreedyPipeline(session, n_slots=4)
+    try:
+        sched = [["A", "B"], ["A", "B", "C"], ["A", "C"], ["A", "B", "C"], ["B"], ["A", "B", "C"]]
+        audio = {k: [_pcm(rng, 1)[0] for _ in range(6)] for k in "ABC"}
+        slot = {}
+        used = {k: 0 for k in "ABC"}
+        step_logp = []
+        for names in sched:
+            for k in names:
+                if k not in slot:
+                    slot[k] = pipe.open_stream()
+            chunks = np.stack([audio[k][used[k]] for k in names])
+            phrases = pipe.forward(chunks, [slot[k] for k in names])
+            lp = pipe._logp[:len(names)].cpu().numpy()
+            step_logp.append({k: lp[i] for i, k in enumerate(names)})
+            for i, k in enumerate(names):
+                used[k] += 1
+            assert len(phrases) == len(names)
+        # sequential per-stream reference on the same session (B = 1, device state chain)
+        session.set_frame_info(None)
+        for k in "ABC":
+            state, j = None, 0
+            for rec in step_logp:
+                if k not in rec:
+                    continue
+                logp, state = session.step(torch.from_numpy(audio[k][j][None]).to(session.dev), state)
+                np.testing.assert_allclose(rec[k], logp.cpu().numpy()[0], atol=1e-4, rtol=0)
+                j += 1
+    finally:
+        session.set_frame_info(None)
+
+
+@pytest.mark.gpu
+def test_forward_offline_matches_oracle_decode(session):
+    """Offline decoding of one utterance: phrases from device frame info == the oracle's splitter +
+    greedy decoder run on the device logprobs of the same steps."""
+    import torch
+    rng = np.random.default_rng(3)
+    audio = np.clip(rng.normal(0, 2500, 8000 * 4), -32768, 32767).astype(np.int32)
+    audio[8000:16000] = 0
+    pipe = P.StreamingGreedyPipeline(session, n_slots=2)
+    got = pipe.forward_offline(audio)
+    # replay: same chunks through session.step, oracle decode on the logprobs
+    padded = np.pad(audio, (P.PADDING, P.PADDING))
+    padded = np.pad(padded, (0, -len(padded) % 2400)).reshape(-1, 2400)
+    session.set_frame_info(None)
+    state, st, want = None, None, []
+    for i, ch in enumerate(padded):
+        logp, state = session.step(torch.from_numpy(ch[None]).to(session.dev), state)
+        out, st = O.pipeline_step(logp.cpu().numpy()[0], st, i == len(padded) - 1)
+        want += out
+    assert [(p.text, p.start_time, p.end_time) for p in got] == want
