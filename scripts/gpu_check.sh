@@ -10,7 +10,7 @@ run() {  # name, limit, command...
   if [ $rc -gt 1 ]; then exit $rc; fi
 }
 run smoke 300 python __graft_entry__.py smoke
-run pytest_gpu 900 python -m pytest tests -m gpu -q -rA
+run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -rA
 run bench 300 python bench.py --steps 20 --warmup 3 --cpu-baseline-s 10
 if [ "${PROFILE:-1}" = 1 ]; then
   run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-baseline-s 0
