@@ -929,9 +929,13 @@ static hipError_t launch_glds_epi(const GemmArgs& a, int epi, int nsplit, hipStr
   }
 }
 
-// bf16 operands already in memory: LDS-DMA kernel
+// bf16 operands already in memory: LDS-DMA kernels
 static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   constexpr int kTarget = 512;
+  // large batches: the persistent transposed-orientation kernels (gemm_t.hip, tools/gemm_bench sweep)
+  const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
+  if (epi == EPI_SWIGLU && a.N % 256 == 0 && t256 >= 192) return gemm_t(a, epi, 0, st);
+  if (epi == EPI_GLU && a.N % 128 == 0 && (int64_t)((a.M + 127) / 128) * (a.N / 128) >= 512) return gemm_t(a, epi, 5, st);
   const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);
   const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
   // 8 waves of 32x64 per 128x128 tile once there is a tile per CU (tools/gemm_bench sweep)

@@ -1,0 +1,494 @@
+// Persistent bf16 GEMM for the large-batch encoder projections, computed in the transposed
+// orientation  D[n][m] = W[n][:] . X[m][:]  (n = output feature, m = frame row of the batch).
+//
+// Why transposed: in the v_mfma_f32_32x32x16_bf16 D layout each lane owns one column (here: one
+// frame row m) and 4-element runs of rows (here: 4 consecutive output features), so the epilogue
+// holds whole 8-byte bf16 / 16-byte fp32 runs of an output row per lane.  A v_permlane32_swap pair
+// widens the bf16 runs to 16-byte stores.  The folded RMSNorm row scale is one value per lane.
+//
+// Structure (MI355X, one 8-wave workgroup per CU, 2 waves per SIMD):
+//   * tile BNW x BMX (256 x 256 for the FFN up-projection, 128 x 256 for N = 384), BK = 64;
+//   * both operands staged into LDS by global_load_lds_dwordx4 (1 KiB per wave instruction =
+//     8 rows x 128 B), two 64 KiB stages, the DMA of K-step g+1 in flight while the MFMAs of
+//     K-step g run; the XOR swizzle slot ^= (row >> 1) & 7 (applied to the per-lane SOURCE address)
+//     makes every ds_read_b128 fragment read conflict-free for the 32x32x16 lane map;
+//   * persistent over tiles: the K-step ring runs across tile boundaries, so the first K-step of
+//     tile t+1 is already in LDS when tile t's epilogue runs (no per-tile prologue bubble);
+//     tiles are dealt XCD-contiguously (an XCD's 32 CUs walk neighbouring tiles: the X row block
+//     is fetched into that XCD's L2 once and reused by every N-tile);
+//   * the bias vector lives in LDS for the whole launch and the row scales go through LDS, so the
+//     epilogue issues no global load that would make hipcc drain the in-flight LDS-DMA.
+// Epilogues (reference ops, see gemm.hip): STORE (+bias, bf16 out), RESID (fp32 R + alpha*(.),
+// fp32 out + bf16 shadow), SWIGLU / GLU on W rows interleaved in 32-row blocks.
+#include "common.h"
+#include "kernels.h"
+
+namespace tone {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBiasMax = 3072;   // largest N of the encoder (FFN up: W1|Wv)
+
+template <int BNW_, int BMX_, int WN_, int WM_>
+struct TT {
+  static constexpr int BNW = BNW_, BMX = BMX_, WN = WN_, WM = WM_;
+};
+
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+}
+
+__device__ __forceinline__ float sumsq8(bf16x8 v, float acc) {
+  const bf16x2 p0 = __builtin_shufflevector(v, v, 0, 1), p1 = __builtin_shufflevector(v, v, 2, 3);
+  const bf16x2 p2 = __builtin_shufflevector(v, v, 4, 5), p3 = __builtin_shufflevector(v, v, 6, 7);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(p0, p0, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(p1, p1, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(p2, p2, acc, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(p3, p3, acc, false);
+}
+
+// bf16-output activations: v_exp_f32 + v_rcp_f32 (~1 ulp fp32, far below the bf16 rounding of the
+// result) instead of the IEEE expf / division sequences
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+__device__ __forceinline__ float fast_silu(float x) { return x * fast_sigmoid(x); }
+
+__device__ __forceinline__ void barrier_lds() {   // keeps LDS-DMA in flight (no vmcnt(0) fence)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// 16 values of one 32x32 D tile for this lane (row m fixed; columns c + (r&3) + 8(r>>2) + 4h) as
+// bf16: pack to 4-element runs, swap runs between the lane halves (T21) so each lane owns 8
+// contiguous elements, and store 2 x 16 B.  rowp points at column c of row m.  All lanes must
+// execute the swaps; only the store is predicated.
+__device__ __forceinline__ void store_tile_bf16(uint16_t* rowp, const float (&v)[16], int lh, bool ok) {
+  uint32_t px[4], py[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    px[g] = pk2(v[4 * g], v[4 * g + 1]);
+    py[g] = pk2(v[4 * g + 2], v[4 * g + 3]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k += 2) {
+    const auto rx = __builtin_amdgcn_permlane32_swap(px[k], px[k + 1], false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(py[k], py[k + 1], false, false);
+    const u32x4 o = {rx[0], ry[0], rx[1], ry[1]};
+    if (ok) *reinterpret_cast<u32x4*>(rowp + 8 * k + 8 * lh) = o;
+  }
+}
+
+// Per-tile epilogue shared by both kernels.  acc[i][j] is the wave's 32x32 D tile (n-tile i,
+// m-tile j); rd[m - m0] the row-scale denominators, sb[n - n0] the bias (both LDS).
+template <int EPI, bool RS, int TI, int TJ, int WTN, int WTM>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[TI][TJ], const float* rd, const float* sb,
+                                              int m0, int n0, int wn, int wm, int lr, int lh) {
+  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int ml = wm * WTM + 32 * j + lr, m = m0 + ml;
+    const bool ok = m < p.M;
+    const int64_t mrow = min(m, p.M - 1);
+    const float inv = RS ? 1.0f / rd[ml] : 1.0f;
+    if constexpr (PAIRED) {
+#pragma unroll
+      for (int ip = 0; ip < TI / 2; ++ip) {
+        const int nl = wn * WTN + 64 * ip;                   // g rows nl..nl+31, u rows nl+32..nl+63
+        float o[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int n = nl + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const float g = fmaf(acc[2 * ip][j][r], inv, sb[n]);
+          const float u = fmaf(acc[2 * ip + 1][j][r], inv, sb[n + 32]);
+          o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
+        }
+        if (p.c_bf16) {
+          store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, o, lh, ok);
+        } else {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 w = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + (n0 + nl) / 2 + 8 * g + 4 * lh) = w;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int nl = wn * WTN + 32 * i, nb = n0 + nl;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = fmaf(acc[i][j][r], inv, sb[nl + (r & 3) + 8 * (r >> 2) + 4 * lh]);
+        if constexpr (EPI == EPI_RESID) {
+          f32x4 rr[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) rr[g] = *reinterpret_cast<const f32x4*>(p.R + mrow * p.ldr + nb + 8 * g + 4 * lh);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4 o;
+            o.x = rr[g].x + p.alpha * v[4 * g];
+            o.y = rr[g].y + p.alpha * v[4 * g + 1];
+            o.z = rr[g].z + p.alpha * v[4 * g + 2];
+            o.w = rr[g].w + p.alpha * v[4 * g + 3];
+            v[4 * g] = o.x; v[4 * g + 1] = o.y; v[4 * g + 2] = o.z; v[4 * g + 3] = o.w;
+            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
+          }
+          if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);
+        } else if (p.c_bf16) {
+          store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + nb, v, lh, ok);
+        } else {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 o = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <class TL, int EPI, bool RS>
+__global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_t_kernel(GemmArgs p) {
+  constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, NW = WN * WM, NT = NW * 64;
+  constexpr int BK = 64, WTN = BNW / WN, WTM = BMX / WM, TI = WTN / 32, TJ = WTM / 32;
+  constexpr int WP = BNW / 8 / NW, XP = BMX / 8 / NW;          // DMA wave-instructions per stage
+  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
+  static_assert(WP >= 1 && XP >= 1 && BNW % (8 * NW) == 0 && BMX % (8 * NW) == 0, "tile/wave mismatch");
+  static_assert(TI >= 1 && TJ >= 1, "wave tile >= 32x32");
+  static_assert(!PAIRED || (TI % 2 == 0), "paired epilogues pair 32-row W blocks");
+  static_assert(EPI == EPI_STORE || EPI == EPI_RESID || PAIRED, "STORE/RESID/SWIGLU/GLU");
+  constexpr int STAGE = (BNW + BMX) * BK;                       // bf16 elements per stage
+  // ONE LDS object: [2 stages][W rows | X rows][64] bf16, rden [2][BMX] fp32, bias [kBiasMax] fp32
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE + 2 * (2 * BMX) + 2 * kBiasMax];
+  float* rden = reinterpret_cast<float*>(lds + 2 * STAGE);
+  float* sbias = rden + 2 * BMX;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid / WM, wm = wid % WM;
+  const int lr = lane & 31, lh = lane >> 5, cs = (lr >> 1) & 7;
+  const int ntn = p.N / BNW, ntm = (p.M + BMX - 1) / BMX, ntiles = ntn * ntm;
+  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int q = (ntiles + 7) >> 3, tbeg = xcd * q, tend = min(ntiles, tbeg + q);
+  const int nmine = (tbeg + jb < tend) ? (tend - tbeg - jb + nxb - 1) / nxb : 0;
+  if (nmine <= 0) return;                                       // workgroup-uniform
+  const int nk = p.K / BK, G = nmine * nk;
+  const uint16_t* __restrict__ X = static_cast<const uint16_t*>(p.A);
+  const uint16_t* __restrict__ W = static_cast<const uint16_t*>(p.W);
+  constexpr bool rs_on = RS;
+
+  for (int i = tid; i < p.N; i += NT) sbias[i] = p.bias ? p.bias[i] : 0.f;
+  __syncthreads();                                              // no DMA in flight yet
+
+  auto tile_of = [&](int g, int& m0, int& n0) {
+    const int t = tbeg + jb + (g / nk) * nxb;
+    m0 = (t / ntn) * BMX;
+    n0 = (t % ntn) * BNW;
+  };
+  auto stage = [&](int buf, int g) {
+    int m0, n0;
+    tile_of(g, m0, n0);
+    const int k0 = (g % nk) * BK;
+    uint16_t* base = lds + buf * STAGE;
+    (void)base;
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int piece = wid + i * NW, row = piece * 8 + (lane >> 3);
+      const uint16_t* src = W + (int64_t)(n0 + row) * p.K + k0 + (((lane & 7) ^ ((row >> 1) & 7)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + piece * 8 * BK, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int piece = wid + i * NW, row = piece * 8 + (lane >> 3);
+      const int gm = min(m0 + row, p.M - 1);
+      const uint16_t* src = X + (int64_t)gm * p.lda + k0 + (((lane & 7) ^ ((row >> 1) & 7)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + (BNW + piece * 8) * BK, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+
+  f32x16 acc[TI][TJ];
+  float ss[TJ];
+  auto zero = [&]() {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      ss[j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
+  };
+
+  // One K-step on LDS buffer buf: every fragment of the step is read first (one counted LDS
+  // wait per slice), then the MFMAs.
+  auto compute = [&](int buf) {
+    const uint16_t* base = lds + buf * STAGE;
+    bf16x8 fa[BK / 16][TI], fb[BK / 16][TJ];
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int off = ((2 * ks + lh) ^ cs) << 3;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        fb[ks][j] = *reinterpret_cast<const bf16x8*>(base + (BNW + wm * WTM + 32 * j + lr) * BK + off);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        fa[ks][i] = *reinterpret_cast<const bf16x8*>(base + (wn * WTN + 32 * i + lr) * BK + off);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (hipcc sinks them to their uses)
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+      if constexpr (RS) {   // m-tile (wn % TJ)'s sum of squares (branch-free select on the uniform wn)
+        bf16x8 bs = fb[ks][0];
+#pragma unroll
+        for (int j = 1; j < TJ; ++j) bs = (wn % TJ == j) ? fb[ks][j] : bs;
+        ss[0] = sumsq8(bs, ss[0]);
+      }
+    }
+  };
+
+  auto epilogue = [&](int m0, int n0, const float* rd) {
+    tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rd, sbias + n0, m0, n0, wn, wm, lr, lh);
+  };
+
+  auto publish_rden = [&](int par) {   // last K-step of a tile: row-scale denominators -> LDS
+    const float t = ss[0] + __shfl_xor(ss[0], 32, 64);
+    if (wn < TJ && lh == 0) rden[par * BMX + wm * WTM + 32 * (wn % TJ) + lr] = sqrtf(t) * p.inv_sqrt_k + kRmsEps;
+  };
+
+  zero();
+  stage(0, 0);
+  for (int g = 0; g < G; ++g) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage g landed (and the last epilogue's stores)
+    barrier_lds();                                      // ... for every wave; buffer (g+1)&1 is free
+    if (g > 0 && g % nk == 0) {                         // previous tile done: its epilogue first
+      int m0, n0;
+      tile_of(g - 1, m0, n0);
+      if (!(p.dbg & 1)) epilogue(m0, n0, rden + ((g / nk - 1) & 1) * BMX);
+      zero();
+    }
+    if (g + 1 < G && !(p.dbg & 4)) stage((g + 1) & 1, g + 1);
+    if (!(p.dbg & 2)) compute(g & 1);
+    if (rs_on && g % nk == nk - 1) publish_rden((g / nk) & 1);
+  }
+  barrier_lds();
+  {
+    int m0, n0;
+    tile_of(G - 1, m0, n0);
+    if (!(p.dbg & 1)) epilogue(m0, n0, rden + ((G / nk - 1) & 1) * BMX);
+    else if (acc[0][0][0] == 1234.5f) static_cast<float*>(p.C)[tid] = acc[TI - 1][TJ - 1][15];   // keep the MFMAs
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two workgroups per CU: 4 waves (2 n x 2 m), tile BNW x BMX (256 x 128: wave tile 128 x 64),
+// BK = 32 (64-byte LDS rows, swizzle slot ^= (row >> 2) & 3, conflict-free for the 32x32x16
+// fragment reads), three LDS-DMA stages (two K-steps in flight).  One tile per workgroup; the two
+// co-resident workgroups drift out of phase, so one's epilogue VALU and DMA waits overlap the
+// other's MFMAs.  LDS per workgroup: 3 x 24 KiB stages + 1 KiB bias + 0.5 KiB row scales.
+template <class TL, int EPI, bool RS>
+__global__ void __launch_bounds__(256) gemm_t2_kernel(GemmArgs p) {
+  constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, NW = WN * WM, NT = NW * 64;
+  constexpr int BK = 32, S = 3, WTN = BNW / WN, WTM = BMX / WM, TI = WTN / 32, TJ = WTM / 32;
+  constexpr int WP = BNW / 16 / NW, XP = BMX / 16 / NW, IPS = WP + XP;    // DMA wave-instructions per stage
+  static_assert(NW == 4 && WP >= 1 && XP >= 1 && BNW % (16 * NW) == 0 && BMX % (16 * NW) == 0, "tile/wave mismatch");
+  static_assert(WN >= TJ, "row-scale ownership: one m-tile per wave");
+  constexpr int STAGE = (BNW + BMX) * BK;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * STAGE + 2 * BNW + 2 * BMX];
+  float* sbias = reinterpret_cast<float*>(lds + S * STAGE);
+  float* rden = sbias + BNW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid / WM, wm = wid % WM;
+  const int lr = lane & 31, lh = lane >> 5, cs = (lr >> 2) & 3;
+  const int ntn = p.N / BNW;
+  int wgid = blockIdx.x;
+  {   // XCD-aware bijective remap: consecutive tiles (same X rows, all N-tiles) share an XCD's L2
+    const int nwg = gridDim.x, xcd = wgid & 7, q = nwg >> 3, rr = nwg & 7;
+    wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
+  }
+  const int m0 = (wgid / ntn) * BMX, n0 = (wgid % ntn) * BNW;
+  const int nk = p.K / BK;
+  const uint16_t* __restrict__ X = static_cast<const uint16_t*>(p.A);
+  const uint16_t* __restrict__ W = static_cast<const uint16_t*>(p.W);
+
+  for (int i = tid; i < BNW; i += NT) sbias[i] = p.bias ? p.bias[n0 + i] : 0.f;
+  __syncthreads();                                              // before any DMA is in flight
+
+  auto stage = [&](int buf, int kt) {
+    const int k0 = kt * BK;
+    uint16_t* base = lds + buf * STAGE;
+    (void)base;
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int piece = wid + i * NW, row = piece * 16 + (lane >> 2);
+      const uint16_t* src = W + (int64_t)(n0 + row) * p.K + k0 + (((lane & 3) ^ ((row >> 2) & 3)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + piece * 16 * BK, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int piece = wid + i * NW, row = piece * 16 + (lane >> 2);
+      const int gm = min(m0 + row, p.M - 1);
+      const uint16_t* src = X + (int64_t)gm * p.lda + k0 + (((lane & 3) ^ ((row >> 2) & 3)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + (BNW + piece * 16) * BK, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float ss = 0.f;
+
+  auto compute = [&](int buf) {
+    const uint16_t* base = lds + buf * STAGE;
+    bf16x8 fa[BK / 16][TI], fb[BK / 16][TJ];
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int off = ((2 * ks + lh) ^ cs) << 3;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        fb[ks][j] = *reinterpret_cast<const bf16x8*>(base + (BNW + wm * WTM + 32 * j + lr) * BK + off);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        fa[ks][i] = *reinterpret_cast<const bf16x8*>(base + (wn * WTN + 32 * i + lr) * BK + off);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+      if constexpr (RS) {
+        bf16x8 bs = fb[ks][0];
+#pragma unroll
+        for (int j = 1; j < TJ; ++j) bs = (wn % TJ == j) ? fb[ks][j] : bs;
+        ss = sumsq8(bs, ss);
+      }
+    }
+  };
+
+  stage(0, 0);
+  if (nk > 1) stage(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPS) : "memory");   // stage kt landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds();                        // visible to all waves; buffer (kt + 2) % S is free
+    if (kt + 2 < nk) stage((kt + 2) % S, kt + 2);
+    compute(kt % S);
+  }
+  if constexpr (RS) {
+    const float t = ss + __shfl_xor(ss, 32, 64);
+    if (wn < TJ && lh == 0) rden[wm * WTM + 32 * (wn % TJ) + lr] = sqrtf(t) * p.inv_sqrt_k + kRmsEps;
+    barrier_lds();
+  }
+  tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
+}
+
+int num_cus_t() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <class TL, int EPI>
+hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
+  static_assert(TL::WN >= TL::BMX / TL::WM / 32, "row-scale ownership: one m-tile per wave");
+  const int ntiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
+  int grid = num_cus_t();
+  const int need = ((ntiles + 7) / 8) * 8;
+  if (grid > need) grid = need;
+  grid = (grid + 7) / 8 * 8;
+  if (a.rowscale) hipLaunchKernelGGL((gemm_t_kernel<TL, EPI, true>), dim3(grid), dim3(TL::WN * TL::WM * 64), 0, st, a);
+  else hipLaunchKernelGGL((gemm_t_kernel<TL, EPI, false>), dim3(grid), dim3(TL::WN * TL::WM * 64), 0, st, a);
+  return hipGetLastError();
+}
+
+template <class TL>
+hipError_t launch_t_epi(const GemmArgs& a, int epi, hipStream_t st) {
+  if (a.N % TL::BNW || a.K % 64 || a.N > kBiasMax || a.rpg || a.M <= 0) return hipErrorInvalidValue;
+  if (a.ldc % 8) return hipErrorInvalidValue;   // 16-byte epilogue stores
+  switch (epi) {
+    case EPI_STORE: return launch_t<TL, EPI_STORE>(a, st);
+    case EPI_RESID: return a.c_bf16 ? hipErrorInvalidValue : launch_t<TL, EPI_RESID>(a, st);
+    case EPI_SWIGLU: return launch_t<TL, EPI_SWIGLU>(a, st);
+    case EPI_GLU: return launch_t<TL, EPI_GLU>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+template <class TL, int EPI>
+hipError_t launch_t2(const GemmArgs& a, hipStream_t st) {
+  const int tiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
+  if (a.rowscale) hipLaunchKernelGGL((gemm_t2_kernel<TL, EPI, true>), dim3(tiles), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((gemm_t2_kernel<TL, EPI, false>), dim3(tiles), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+template <class TL>
+hipError_t launch_t2_epi(const GemmArgs& a, int epi, hipStream_t st) {
+  if (a.N % TL::BNW || a.K % 32 || a.rpg || a.M <= 0) return hipErrorInvalidValue;
+  if (a.ldc % 8) return hipErrorInvalidValue;   // 16-byte epilogue stores
+  switch (epi) {
+    case EPI_STORE: return launch_t2<TL, EPI_STORE>(a, st);
+    case EPI_RESID: return a.c_bf16 ? hipErrorInvalidValue : launch_t2<TL, EPI_RESID>(a, st);
+    case EPI_SWIGLU: return launch_t2<TL, EPI_SWIGLU>(a, st);
+    case EPI_GLU: return launch_t2<TL, EPI_GLU>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// Tile variants: 0 = 256x256 (waves 2x4), 1 = 128x256 (2x4), 2 = 256x128 (2x4), 3 = 128x128 (2x4)
+hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st) {
+  if (!a.a_bf16) return hipErrorInvalidValue;
+  switch (variant) {
+    case 0: return launch_t_epi<TT<256, 256, 2, 4>>(a, epi, st);
+    case 1: return launch_t_epi<TT<128, 256, 2, 4>>(a, epi, st);
+    case 2: return launch_t_epi<TT<256, 128, 2, 4>>(a, epi, st);
+    case 3: return launch_t_epi<TT<128, 128, 2, 4>>(a, epi, st);
+    case 4: return launch_t2_epi<TT<256, 128, 2, 2>>(a, epi, st);   // 2 workgroups per CU
+    case 5: return launch_t2_epi<TT<128, 128, 2, 2>>(a, epi, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tone

@@ -25,14 +25,20 @@ __device__ float bf(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 // naive reference: out[m][o] for the epilogue (no rowscale)
 __global__ void ref_kernel(const uint16_t* A, const uint16_t* W, const float* bias, const float* R, float* out, int M,
-                           int N, int K, int epi) {
+                           int N, int K, int epi, int rowscale) {
   const int m = blockIdx.y, o = blockIdx.x * blockDim.x + threadIdx.x;
   const int nout = (epi >= 2) ? N / 2 : N;
   if (o >= nout) return;
+  float den = 1.f;
+  if (rowscale) {
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += bf(A[(int64_t)m * K + k]) * bf(A[(int64_t)m * K + k]);
+    den = sqrtf(s) / sqrtf((float)K) + 1e-8f;
+  }
   auto dot = [&](int n) {
     float acc = 0.f;
     for (int k = 0; k < K; ++k) acc += bf(A[(int64_t)m * K + k]) * bf(W[(int64_t)n * K + k]);
-    return acc + bias[n];
+    return acc / den + bias[n];
   };
   float v;
   if (epi <= 1) {
@@ -94,23 +100,29 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(W, hW.data(), hW.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(bias, hb.data(), N * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(R, hR.data(), hR.size() * 4, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(ref_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, A, W, bias, R, ref, M, N, K, epi);
+  const int rowscale = getenv("ROWSCALE") ? atoi(getenv("ROWSCALE")) : 0;
+  hipLaunchKernelGGL(ref_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, A, W, bias, R, ref, M, N, K, epi, rowscale);
   CK(hipDeviceSynchronize());
 
   GemmArgs a{};
   a.A = A; a.lda = K; a.W = W; a.C = C; a.ldc = nout; a.bias = bias; a.R = R; a.ldr = N; a.alpha = 1.f;
   a.M = M; a.N = N; a.K = K; a.ws = ws; a.ws_cap = ws_cap; a.a_bf16 = 1; a.c_bf16 = cbf;
   a.C2 = epi == 1 ? C2 : nullptr;
+  a.rowscale = rowscale;
+  a.inv_sqrt_k = 1.0f / sqrtf((float)K);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const double flop = 2.0 * M * N * (double)K;
   char* list = strdup(argv[5]);
   for (char* tok = strtok(list, ","); tok; tok = strtok(nullptr, ",")) {
     const int vv = atoi(tok);
-    const int v = vv < 0 ? vv : (vv & 15);     // +16: N-partitioned XCD order, +32: non-temporal stores
-    a.order_n = vv >= 0 && (vv & 16);
-    a.nt_store = vv >= 0 && (vv & 32);
-    a.dbg = vv >= 0 ? (vv >> 6) & 7 : 0;      // +64 no epilogue, +128 no MFMA, +256 no K loop
+    // v % 100 = variant (20..23: gemm_t tiles); (v / 100) bits: 1 N-partitioned XCD order,
+    // 2 non-temporal stores, 4.. debug (no epilogue / no K loop)
+    const int v = vv < 0 ? vv : (vv % 100);
+    const int fl = vv < 0 ? 0 : vv / 100;
+    a.order_n = fl & 1;
+    a.nt_store = (fl >> 1) & 1;
+    a.dbg = (fl >> 2) & 7;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
     const bool f32 = (vv == -2);
@@ -118,7 +130,9 @@ int main(int argc, char** argv) {
     a.W = f32 ? (const void*)Wf : (const void*)W;
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
-    auto launch = [&]() { return v < 0 ? gemm(a, epi, !f32, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0); };
+    auto launch = [&]() {
+      return v < 0 ? gemm(a, epi, !f32, 0) : v >= 20 ? gemm_t(a, epi, v - 20, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0);
+    };
     hipError_t rc = launch();
     if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", v, hipGetErrorString(rc)); continue; }
     CK(hipDeviceSynchronize());

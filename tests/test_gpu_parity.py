@@ -241,3 +241,25 @@ def test_bf16_mode_close_to_oracle(weights, oracle):
     s.close()
     assert worst < 0.25, worst
     assert np.mean(agree) > 0.97, agree
+
+
+def test_bf16_large_batch_paths(weights, oracle):
+    """bf16 at a batch large enough for the persistent / two-workgroup GEMM paths (M = 20480 rows):
+    a sample of the streams against the oracle, same bounds as the small-batch bf16 check."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    b, pick = 2048, np.arange(0, 2048, 64)
+    s = ToneSession(weights, precision="bf16", max_batch=b)
+    rng = np.random.default_rng(17)
+    st = np.zeros((b, C.STATE_SIZE), np.float16)
+    st_o = np.zeros((len(pick), C.STATE_SIZE), np.float16)
+    agree, worst = [], 0.0
+    for c in range(2):
+        pcm = synthetic_pcm(rng, b)
+        lp_g, st = gpu_step(s, pcm, st)
+        lp_o, st_o = oracle.step(pcm[pick], st_o)
+        worst = max(worst, float(np.abs(lp_g[pick] - lp_o).max()))
+        agree.append(np.mean(lp_g[pick].argmax(-1) == lp_o.argmax(-1)))
+    s.close()
+    assert worst < 0.25, worst
+    assert np.mean(agree) > 0.97, agree
