@@ -90,150 +90,159 @@ hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, i
 
 // ---------------------------------------------------------------------------------------------
 // RotaryMultiHeadAttention.forward (conformer_blocks.py:688-726) + forward_qkv/forward_attention
-// (submodules.py:204-271).  One 256-thread workgroup per (stream, group of 2 heads):
-//   recompute: q,k -> per-head LayerNorm(48) -> RoPE on dims [0,32) (q at positions 0..T-1, k at
-//              -S..T-1) -> scores = q.k^T / sqrt(48) -> mask (layers 14/15) -> softmax
-//   shared   : probabilities of the last recomputing layer (scores are shared and no mask applies
-//              to layers 1-6 / 8-13, so softmax(shared scores) = shared probabilities)
-//   ctx = P . V
-// LayerNorm+RoPE use 16 lanes per (row, head): lane l owns dims l, l+16 (a RoPE pair) and 32+l.
+// (submodules.py:204-271).  One wave per (stream, head), four heads per 256-thread workgroup;
+// every wave works in its own small LDS slice, so the kernel has no workgroup barrier.  T (query
+// rows) and S (cached rows; TK = S + T keys) are template parameters so every per-lane array stays
+// in registers.
+//   recompute: key row j lives in lane j (its 48 dims in registers): per-head LayerNorm(48,
+//              eps 1e-5) and RoPE on dims [0,32) (rotate_half pairs d, d+16; k at positions
+//              -S..T-1) run in-lane; the T query rows get the same treatment in lanes 0..T-1 and
+//              go to LDS; lane j then computes scores q_i . k_j / sqrt(48) for every i, applies the
+//              layer 14/15 masks, and the softmax over j is a wave reduction per query row.
+//   shared   : probabilities of the last recomputing layer (no mask in layers 1-6 / 8-13, so
+//              softmax(shared scores) = shared probabilities), read from the probs buffer.
+//   ctx = P . V: lane c < 48 owns output column c; its TK values of V are loaded straight into
+//   registers at kernel start (one coalesced row per load), P rows are read from LDS as
+//   broadcast float4s, the T output rows accumulate independently.
 constexpr int kMaxT = 10, kMaxTK = 40;
-constexpr int kHG = 2;                       // heads per workgroup
-constexpr int kHC = kHG * kDk;               // 96 columns per workgroup
 
-template <bool OBF>
+template <int T, int S, bool REC, bool OBF>
 __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = blockIdx.x / (kHeads / kHG), hg = blockIdx.x % (kHeads / kHG);
-  const int c0 = hg * kHC, tid = threadIdx.x;
-  const int T = a.T, S = a.S, TK = S + T;
-  float* qs = sm;                    // [T][96]
-  float* ks = qs + T * kHC;          // [TK][96]
-  float* vs = ks + TK * kHC;         // [TK][96]
-  float* ps = vs + TK * kHC;         // [2][T][TK]
-  constexpr int C4 = kHC / 4;
-  for (int e = tid; e < TK * C4; e += 256) {
-    const int j = e / C4, c4 = e % C4;
-    *reinterpret_cast<float4*>(vs + j * kHC + 4 * c4) =
-        *reinterpret_cast<const float4*>(a.v + ((int64_t)b * TK + j) * a.ldv + c0 + 4 * c4);
-  }
-  if (a.recompute) {
-    for (int e = tid; e < T * C4; e += 256) {
-      const int j = e / C4, c4 = e % C4;
-      *reinterpret_cast<float4*>(qs + j * kHC + 4 * c4) =
-          *reinterpret_cast<const float4*>(a.q + ((int64_t)b * T + j) * a.ldq + c0 + 4 * c4);
-    }
-    for (int e = tid; e < TK * C4; e += 256) {
-      const int j = e / C4, c4 = e % C4;
-      *reinterpret_cast<float4*>(ks + j * kHC + 4 * c4) =
-          *reinterpret_cast<const float4*>(a.k + ((int64_t)b * TK + j) * a.ldk + c0 + 4 * c4);
-    }
-    __syncthreads();
-    // per-head LayerNorm (eps 1e-5) + partial RoPE: 16 lanes per (row, head)
-    const int l = tid & 15;
-    const int npairs = (T + TK) * kHG;
-    for (int pr = tid >> 4; pr < ((npairs + 15) & ~15); pr += 16) {
-      const bool live = pr < npairs;
-      const int r = live ? pr / kHG : 0, hl = pr % kHG;
-      const bool isq = r < T;
-      float* base = (isq ? qs + r * kHC : ks + (r - T) * kHC) + hl * kDk;
-      const float* lw = isq ? a.qln_w : a.kln_w;
-      const float* lb = isq ? a.qln_b : a.kln_b;
-      const float x0 = base[l], x1 = base[l + 16], x2 = base[l + 32];
-      float sum = x0 + x1 + x2;
+  constexpr int TK = S + T, TKP = (TK + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) float sm[4][T * kDk + T * TKP];
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int b = blockIdx.x >> 1, h = ((blockIdx.x & 1) << 2) + wid;
+  float* qs = sm[wid];                        // [T][48]
+  float* ps = qs + T * kDk;                   // [T][TKP]
+  const int c0 = h * kDk;
+  const int cl = min(lane, kDk - 1);
+  float vr[TK];                               // V column cl, all keys (issued first: in flight meanwhile)
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-      const float mu = sum / (float)kDk;
-      const float d0 = x0 - mu, d1 = x1 - mu, d2 = x2 - mu;
-      float var = d0 * d0 + d1 * d1 + d2 * d2;
+  for (int j = 0; j < TK; ++j) vr[j] = a.v[((int64_t)b * TK + j) * a.ldv + c0 + cl];
+  if constexpr (REC) {
+    // LayerNorm + RoPE of one 48-dim row held in registers; pos = RoPE position
+    auto ln_rope = [&](float (&x)[kDk], const float* lw, const float* lb, int pos) {
+      float mu = 0.f;
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) var += __shfl_xor(var, o, 64);
-      var /= (float)kDk;
-      const float rstd = 1.0f / sqrtf(var + kLnEps);
-      const float y0 = d0 * rstd * lw[l] + lb[l];
-      const float y1 = d1 * rstd * lw[l + 16] + lb[l + 16];
-      const float y2 = d2 * rstd * lw[l + 32] + lb[l + 32];
-      const int pos = isq ? r : (r - T) - S;
-      const float cs = a.rope_cos[(pos + kMhsaS) * (kRope / 2) + l];
-      const float sn = a.rope_sin[(pos + kMhsaS) * (kRope / 2) + l];
-      if (live) {
-        base[l] = y0 * cs - y1 * sn;            // rotate_half pairs (l, l+16), submodules.py:142-157
-        base[l + 16] = y1 * cs + y0 * sn;
-        base[l + 32] = y2;
+      for (int d = 0; d < kDk; ++d) mu += x[d];
+      mu *= (1.0f / kDk);
+      float var = 0.f;
+#pragma unroll
+      for (int d = 0; d < kDk; ++d) {
+        x[d] -= mu;
+        var += x[d] * x[d];
       }
+      const float rstd = 1.0f / sqrtf(var * (1.0f / kDk) + kLnEps);
+#pragma unroll
+      for (int d = 0; d < kDk; ++d) x[d] = x[d] * rstd * lw[d] + lb[d];
+      const float* cs = a.rope_cos + (pos + kMhsaS) * (kRope / 2);
+      const float* sn = a.rope_sin + (pos + kMhsaS) * (kRope / 2);
+#pragma unroll
+      for (int d = 0; d < kRope / 2; ++d) {            // rotate_half pairs (d, d+16), submodules.py:142-157
+        const float y0 = x[d], y1 = x[d + 16];
+        x[d] = y0 * cs[d] - y1 * sn[d];
+        x[d + 16] = y1 * cs[d] + y0 * sn[d];
+      }
+    };
+    if (lane < T) {   // query rows first (their registers are free again before the key rows load)
+      float qr[kDk];
+#pragma unroll
+      for (int c4 = 0; c4 < kDk / 4; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(a.q + ((int64_t)b * T + lane) * a.ldq + c0 + 4 * c4);
+        qr[4 * c4] = v.x; qr[4 * c4 + 1] = v.y; qr[4 * c4 + 2] = v.z; qr[4 * c4 + 3] = v.w;
+      }
+      ln_rope(qr, a.qln_w, a.qln_b, lane);
+#pragma unroll
+      for (int c4 = 0; c4 < kDk / 4; ++c4)
+        *reinterpret_cast<float4*>(qs + lane * kDk + 4 * c4) = make_float4(qr[4 * c4], qr[4 * c4 + 1], qr[4 * c4 + 2], qr[4 * c4 + 3]);
     }
-    __syncthreads();
+    float kr[kDk];
+    const int jr = min(lane, TK - 1);
+#pragma unroll
+    for (int c4 = 0; c4 < kDk / 4; ++c4) {
+      const float4 v = *reinterpret_cast<const float4*>(a.k + ((int64_t)b * TK + jr) * a.ldk + c0 + 4 * c4);
+      kr[4 * c4] = v.x; kr[4 * c4 + 1] = v.y; kr[4 * c4 + 2] = v.z; kr[4 * c4 + 3] = v.w;
+    }
+    ln_rope(kr, a.kln_w, a.kln_b, jr - S);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float off = -1e30f;
-    if (S > 0) {
+    if constexpr (S > 0) {
       off = (float)kMhsaS - __half2float(a.s.in[a.s.row(b) + kOffMhsaLen]);
       if (a.reduced) off = floorf(off / 2.0f);
     }
-    const int nsc = kHG * T * TK;
-    for (int e = tid; e < nsc; e += 256) {
-      const int hl = e / (T * TK), i = (e / TK) % T, j = e % TK;
-      const float4* q4 = reinterpret_cast<const float4*>(qs + i * kHC + hl * kDk);
-      const float4* k4 = reinterpret_cast<const float4*>(ks + j * kHC + hl * kDk);
+    const bool live = lane < TK;
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      const float4* q4 = reinterpret_cast<const float4*>(qs + i * kDk);
       float acc = 0.f;
 #pragma unroll
-      for (int d = 0; d < kDk / 4; ++d) {
-        const float4 x = q4[d], y = k4[d];
-        acc = fmaf(x.x, y.x, acc);
-        acc = fmaf(x.y, y.y, acc);
-        acc = fmaf(x.z, y.z, acc);
-        acc = fmaf(x.w, y.w, acc);
+      for (int c4 = 0; c4 < kDk / 4; ++c4) {
+        const float4 q = q4[c4];
+        acc = fmaf(q.x, kr[4 * c4], acc);
+        acc = fmaf(q.y, kr[4 * c4 + 1], acc);
+        acc = fmaf(q.z, kr[4 * c4 + 2], acc);
+        acc = fmaf(q.w, kr[4 * c4 + 3], acc);
       }
-      const float sc = acc / 6.928203230275509f;   // / math.sqrt(48) (submodules.py:185, conformer_blocks.py:725)
-      const bool masked = (S > 0) && (((float)j < off) || ((float)(S + i) < off));
-      ps[e] = masked ? -10000.0f : sc;
-    }
-    __syncthreads();
-    for (int rr = tid; rr < kHG * T; rr += 256) {
-      float* row = ps + rr * TK;
-      const int i = rr % T;
-      float m = -INFINITY;
-      for (int j = 0; j < TK; ++j) m = fmaxf(m, row[j]);
-      float sum = 0.f;
-      for (int j = 0; j < TK; ++j) {
-        const float e = expf(row[j] - m);
-        row[j] = e;
-        sum += e;
-      }
-      for (int j = 0; j < TK; ++j) {
-        const bool masked = (S > 0) && (((float)j < off) || ((float)(S + i) < off));
-        row[j] = masked ? 0.f : row[j] / sum;
-      }
-    }
-    __syncthreads();
-    if (a.probs) {
-      for (int e = tid; e < kHG * T * TK; e += 256) {
-        const int hl = e / (T * TK), rem = e % (T * TK);
-        a.probs[(((int64_t)b * kHeads + hg * kHG + hl) * T) * TK + rem] = ps[e];
+      const float sc = acc / 6.928203230275509f;       // / math.sqrt(48) (submodules.py:185)
+      const bool masked = (S > 0) && (((float)lane < off) || ((float)(S + i) < off));
+      const float x = live ? (masked ? -10000.0f : sc) : -INFINITY;
+      const float m = wave_max(x);
+      const float e = live ? expf(x - m) : 0.f;
+      const float sum = wave_sum(e);
+      const float p = masked ? 0.f : e / sum;
+      if (live) {
+        ps[i * TKP + lane] = p;
+        if (a.probs) a.probs[(((int64_t)b * kHeads + h) * T + i) * TK + lane] = p;
       }
     }
   } else {
-    for (int e = tid; e < kHG * T * TK; e += 256) {
-      const int hl = e / (T * TK), rem = e % (T * TK);
-      ps[e] = a.probs[(((int64_t)b * kHeads + hg * kHG + hl) * T) * TK + rem];
-    }
-    __syncthreads();
+    static_assert(S == 0, "shared probabilities only in layers without a cache");
+    const float* pp = a.probs + ((int64_t)b * kHeads + h) * T * TK;
+    for (int e = lane; e < T * TK; e += 64) ps[(e / TK) * TKP + e % TK] = pp[e];
   }
-  for (int e = tid; e < T * kHC; e += 256) {
-    const int i = e / kHC, c = e % kHC, hl = c / kDk;
-    const float* pr = ps + (hl * T + i) * TK;
-    float acc = 0.f;
-    for (int j = 0; j < TK; ++j) acc = fmaf(pr[j], vs[j * kHC + c], acc);
-    store_act<OBF>(a.ctx, ((int64_t)b * T + i) * kD + c0 + c, acc);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float acc[T];
+#pragma unroll
+  for (int i = 0; i < T; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int j4 = 0; j4 < TKP / 4; ++j4) {
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      const float4 p4 = *reinterpret_cast<const float4*>(ps + i * TKP + 4 * j4);
+      acc[i] = fmaf(p4.x, vr[4 * j4], acc[i]);
+      if (4 * j4 + 1 < TK) acc[i] = fmaf(p4.y, vr[4 * j4 + 1], acc[i]);
+      if (4 * j4 + 2 < TK) acc[i] = fmaf(p4.z, vr[4 * j4 + 2], acc[i]);
+      if (4 * j4 + 3 < TK) acc[i] = fmaf(p4.w, vr[4 * j4 + 3], acc[i]);
+    }
+  }
+  if (lane < kDk) {
+#pragma unroll
+    for (int i = 0; i < T; ++i) store_act<OBF>(a.ctx, ((int64_t)b * T + i) * kD + c0 + lane, acc[i]);
   }
 }
 
-hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
-  if (a.T > kMaxT || a.S + a.T > kMaxTK) return hipErrorInvalidValue;
-  const int tk = a.S + a.T;
-  const size_t smem = (size_t)(a.T * kHC + 2 * tk * kHC + kHG * a.T * tk) * sizeof(float);
-  const dim3 grid(a.B * (kHeads / kHG));
-  if (a.ctx_bf16) hipLaunchKernelGGL(attention_kernel<true>, grid, dim3(256), smem, st, a);
-  else hipLaunchKernelGGL(attention_kernel<false>, grid, dim3(256), smem, st, a);
+template <bool OBF>
+static hipError_t launch_attention_t(const AttnArgs& a, hipStream_t st) {
+  const dim3 grid(a.B * 2), block(256);
+  if (!a.recompute) {
+    if (a.S != 0) return hipErrorInvalidValue;
+    if (a.T == 10) hipLaunchKernelGGL((attention_kernel<10, 0, false, OBF>), grid, block, 0, st, a);
+    else if (a.T == 5) hipLaunchKernelGGL((attention_kernel<5, 0, false, OBF>), grid, block, 0, st, a);
+    else return hipErrorInvalidValue;
+  } else if (a.T == 10 && a.S == 0) hipLaunchKernelGGL((attention_kernel<10, 0, true, OBF>), grid, block, 0, st, a);
+  else if (a.T == 5 && a.S == 0) hipLaunchKernelGGL((attention_kernel<5, 0, true, OBF>), grid, block, 0, st, a);
+  else if (a.T == 5 && a.S == 15) hipLaunchKernelGGL((attention_kernel<5, 15, true, OBF>), grid, block, 0, st, a);
+  else if (a.T == 10 && a.S == 30) hipLaunchKernelGGL((attention_kernel<10, 30, true, OBF>), grid, block, 0, st, a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
+  return a.ctx_bf16 ? launch_attention_t<true>(a, st) : launch_attention_t<false>(a, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -380,47 +389,46 @@ hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* sha
 
 // ---------------------------------------------------------------------------------------------
 // ConvASRDecoder.forward (conformer.py:338-354): 1x1 conv 384 -> 35 and log_softmax, fp32.
-// One lane per frame row: the 35 vocabulary dot products accumulate in registers while x streams
-// through in 8-float slices and the (broadcast) weight rows come from LDS; log-softmax, the greedy
-// token and the splitter's speech flag are per-lane epilogues, and the wave's 64 x 35 logprob block
-// (contiguous in memory) leaves through LDS as coalesced stores.
+// Four lanes per frame row (16 rows per wave): lane l owns row l >> 2 and the k quarter l & 3
+// (96 k), so each LDS read of W serves 4 distinct broadcast addresses and x rows stream through
+// L1; the 35 partial sums are combined over the quarter lanes with two xor shuffles, then
+// log-softmax, the greedy token and the splitter's speech flag are per-row epilogues.
 //   frame_info[row] = argmax_v logp[row][v] (first index on ties, decoder.py:57)
 //                   | (exp(logp[33]) + exp(logp[34]) <= 0.9) << 8      (logprob_splitter.py:134)
 constexpr float kSilenceThreshold = 0.9f;
-__global__ void __launch_bounds__(64) head_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                  const float* __restrict__ bias, float* __restrict__ logp,
-                                                  int32_t* __restrict__ frame_info, int rows) {
-  __shared__ __attribute__((aligned(16))) float ws[kVocab * kD];
-  __shared__ float lo[64 * kVocab];
-  const int lane = threadIdx.x;
-  for (int i = lane; i < kVocab * kD / 4; i += 64)
-    reinterpret_cast<f32x4_t*>(ws)[i] = reinterpret_cast<const f32x4_t*>(w)[i];
+constexpr int kHeadQ = kD / 4;              // 96
+constexpr int kHeadWs = kHeadQ + 4;         // padded LDS row of a W quarter (bank spread)
+__global__ void __launch_bounds__(256) head_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ bias, float* __restrict__ logp,
+                                                   int32_t* __restrict__ frame_info, int rows) {
+  __shared__ __attribute__((aligned(16))) float ws[4 * kVocab * kHeadWs];   // [quarter][v][96 (+4)]
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < kVocab * kD / 4; i += 256) {
+    const int v = (4 * i) / kD, k = (4 * i) % kD, q = k / kHeadQ, kk = k % kHeadQ;
+    *reinterpret_cast<f32x4_t*>(ws + (q * kVocab + v) * kHeadWs + kk) = reinterpret_cast<const f32x4_t*>(w)[i];
+  }
   __syncthreads();
-  const int row0 = blockIdx.x * 64, row = row0 + lane;
-  const float* xr = x + (int64_t)min(row, rows - 1) * kD;
+  const int row = blockIdx.x * 64 + (tid >> 2), q = lane & 3;
+  const float* xr = x + (int64_t)min(row, rows - 1) * kD + q * kHeadQ;
+  const float* wq = ws + q * kVocab * kHeadWs;
   float acc[kVocab];
 #pragma unroll
   for (int v = 0; v < kVocab; ++v) acc[v] = 0.f;
-  f32x4_t xa = reinterpret_cast<const f32x4_t*>(xr)[0], xb = reinterpret_cast<const f32x4_t*>(xr)[1];
-  for (int k = 0; k < kD; k += 8) {
-    const f32x4_t ca = xa, cb = xb;
-    if (k + 8 < kD) {
-      xa = reinterpret_cast<const f32x4_t*>(xr + k + 8)[0];
-      xb = reinterpret_cast<const f32x4_t*>(xr + k + 8)[1];
-    }
+  for (int k = 0; k < kHeadQ; k += 4) {
+    const f32x4_t xv = *reinterpret_cast<const f32x4_t*>(xr + k);
 #pragma unroll
     for (int v = 0; v < kVocab; ++v) {
-      const f32x4_t wa = *reinterpret_cast<const f32x4_t*>(ws + v * kD + k);
-      const f32x4_t wb = *reinterpret_cast<const f32x4_t*>(ws + v * kD + k + 4);
+      const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(wq + v * kHeadWs + k);
       float a = acc[v];
-      a = fmaf(wa.x, ca.x, a); a = fmaf(wa.y, ca.y, a); a = fmaf(wa.z, ca.z, a); a = fmaf(wa.w, ca.w, a);
-      a = fmaf(wb.x, cb.x, a); a = fmaf(wb.y, cb.y, a); a = fmaf(wb.z, cb.z, a); a = fmaf(wb.w, cb.w, a);
+      a = fmaf(wv.x, xv.x, a); a = fmaf(wv.y, xv.y, a); a = fmaf(wv.z, xv.z, a); a = fmaf(wv.w, xv.w, a);
       acc[v] = a;
     }
   }
   float m = -INFINITY;
 #pragma unroll
   for (int v = 0; v < kVocab; ++v) {
+    acc[v] += __shfl_xor(acc[v], 1, 64);
+    acc[v] += __shfl_xor(acc[v], 2, 64);
     acc[v] += bias[v];
     m = fmaxf(m, acc[v]);
   }
@@ -430,26 +438,28 @@ __global__ void __launch_bounds__(64) head_kernel(const float* __restrict__ x, c
   const float lse = logf(se);
   float best = -INFINITY;
   int tok = 0;
+  float lp[kVocab];
 #pragma unroll
   for (int v = 0; v < kVocab; ++v) {
-    const float lp = acc[v] - m - lse;
-    lo[lane * kVocab + v] = lp;
-    if (lp > best) { best = lp; tok = v; }
+    lp[v] = acc[v] - m - lse;
+    if (lp[v] > best) { best = lp[v]; tok = v; }
   }
-  if (frame_info && row < rows) {
-    const float sil = expf(lo[lane * kVocab + kVocab - 2]) + expf(lo[lane * kVocab + kVocab - 1]);
-    frame_info[row] = tok | ((sil <= kSilenceThreshold) ? 256 : 0);
+  if (row < rows) {
+    float* dst = logp + (int64_t)row * kVocab;
+#pragma unroll
+    for (int v = 0; v < kVocab; ++v)
+      if ((v & 3) == q) dst[v] = lp[v];                // the 4 quarter lanes split the row's stores
+    if (frame_info && q == 0) {
+      const float sil = expf(lp[kVocab - 2]) + expf(lp[kVocab - 1]);
+      frame_info[row] = tok | ((sil <= kSilenceThreshold) ? 256 : 0);
+    }
   }
-  __syncthreads();
-  const int nrow = min(64, rows - row0);
-  float* dst = logp + (int64_t)row0 * kVocab;
-  for (int i = lane; i < nrow * kVocab; i += 64) dst[i] = lo[i];
 }
 
 hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows,
                        hipStream_t st) {
   if (rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(head_kernel, dim3((rows + 63) / 64), dim3(64), 0, st, x, w, b, logp, frame_info, rows);
+  hipLaunchKernelGGL(head_kernel, dim3((rows + 63) / 64), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
   return hipGetLastError();
 }
 
