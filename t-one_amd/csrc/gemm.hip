@@ -1015,6 +1015,11 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     if (a.K % 64 != 0 || a.N % 128 != 0 || a.M <= 0 || (epi == EPI_RESID && a.c_bf16)) return hipErrorInvalidValue;
     return gemm_bf16(a, epi, st);
   }
+  if (!bf16 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
+    // exact-fp32 projections other than the FFN up-projection: in-workgroup K split (gemm_t.hip)
+    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_f32t(a, epi, 0, st);
+    if (epi == EPI_GLU && a.N % 128 == 0) return gemm_f32t(a, epi, 1, st);
+  }
   if (a.K % bk != 0 || a.N % 128 != 0 || a.M <= 0) return hipErrorInvalidValue;
   if (!bf16 && (a.a_bf16 || a.c_bf16)) return hipErrorInvalidValue;
   if (epi == EPI_RESID && a.c_bf16) return hipErrorInvalidValue;

@@ -417,6 +417,157 @@ __global__ void __launch_bounds__(256) gemm_t2_kernel(GemmArgs p) {
   tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 projections with few output tiles (N = 384..1152 at B = 256: M = 2560 / 1280 frame rows).
+// Exact-fp32 MFMA (v_mfma_f32_32x32x2_f32), transposed orientation like above, one 32x32 (or
+// 32x64) accumulator tile per wave and the K range split over WK wave groups INSIDE the workgroup
+// (partials reduced through LDS at the end) -- enough waves for 1024 SIMDs without a split-K
+// workspace round trip or a second kernel.  K-step = WK x 32: each group's 32-float (128-byte) row
+// slice is its own region of the stage, filled by LDS-DMA with the same slot swizzle as the bf16
+// kernels (fragment reads: lane (row r, half h) takes float4 slot 2q + h, q = 0..3; both operands
+// use the same k permutation, so the 4 MFMAs per float4 pair sum the right products).
+template <int BNW_, int BMX_, int WN_, int WM_, int WK_>
+struct FT {
+  static constexpr int BNW = BNW_, BMX = BMX_, WN = WN_, WM = WM_, WK = WK_;
+};
+
+template <class TL, int EPI, bool RS>
+__global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kernel(GemmArgs p) {
+  constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, WK = TL::WK;
+  constexpr int NW = WN * WM * WK, NT = NW * 64, S = 3;
+  constexpr int WTN = BNW / WN, WTM = BMX / WM, TI = WTN / 32, TJ = WTM / 32;
+  constexpr int GROUP = (BNW + BMX) * 32;                       // floats of one k-group's slice
+  constexpr int STAGE = WK * GROUP;
+  constexpr int PIECES = WK * (BNW + BMX) / 8, IPW = PIECES / NW;  // 1 KiB DMA instructions
+  static_assert(PIECES % NW == 0 && IPW >= 1, "DMA pieces per wave");
+  static_assert(WN >= TJ, "row-scale ownership");
+  constexpr int RED = (WK - 1) * (NW / WK) * 64 * TI * TJ * 16;   // K-split partials (floats)
+  constexpr int LDSF = (S * STAGE > RED ? S * STAGE : RED);
+  __shared__ __attribute__((aligned(16))) float lds[LDSF + BNW + BMX + (WK - 1) * (NW / WK) * 64];
+  float* sbias = lds + LDSF;
+  float* rden = sbias + BNW;
+  float* ssr = rden + BMX;                                      // K-split row sums of squares
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wid / (WN * WM), wr = wid % (WN * WM), wn = wr / WM, wm = wr % WM;
+  const int lr = lane & 31, lh = lane >> 5, cs = (lr >> 1) & 7;
+  const int ntn = p.N / BNW;
+  int wgid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = wgid & 7, q = nwg >> 3, rr = nwg & 7;
+    wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
+  }
+  const int m0 = (wgid / ntn) * BMX, n0 = (wgid % ntn) * BNW;
+  const int nk = p.K / (32 * WK);
+  const float* __restrict__ X = static_cast<const float*>(p.A);
+  const float* __restrict__ W = static_cast<const float*>(p.W);
+
+  for (int i = tid; i < BNW; i += NT) sbias[i] = p.bias ? p.bias[n0 + i] : 0.f;
+  __syncthreads();
+
+  auto stage = [&](int buf, int kt) {
+    float* base = lds + buf * STAGE;
+    (void)base;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int piece = wid + i * NW;                           // 8 rows x 128 B
+      const int g = piece / ((BNW + BMX) / 8), pr = piece % ((BNW + BMX) / 8);
+      const int row = pr * 8 + (lane >> 3);                     // row of [W rows | X rows]
+      const int k0 = (kt * WK + g) * 32 + (((lane & 7) ^ ((row >> 1) & 7)) << 2);
+      const float* src = row < BNW ? W + (int64_t)(n0 + row) * p.K + k0
+                                   : X + (int64_t)min(m0 + row - BNW, p.M - 1) * p.lda + k0;
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + g * GROUP + pr * 8 * 32, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float ss = 0.f;
+  const int jss = wn % TJ;                                      // m-tile whose sum of squares this wave keeps
+
+  auto compute = [&](int buf) {
+    const float* base = lds + buf * STAGE + wk * GROUP;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int off = ((2 * q + lh) ^ cs) << 2;
+      f32x4 fa[TI], fb[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) fa[i] = *reinterpret_cast<const f32x4*>(base + (wn * WTN + 32 * i + lr) * 32 + off);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) fb[j] = *reinterpret_cast<const f32x4*>(base + (BNW + wm * WTM + 32 * j + lr) * 32 + off);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][e], fb[j][e], acc[i][j], 0, 0, 0);
+      if constexpr (RS) {
+        f32x4 v = fb[0];
+#pragma unroll
+        for (int j = 1; j < TJ; ++j) v = (jss == j) ? fb[j] : v;
+        ss = fmaf(v.x, v.x, ss); ss = fmaf(v.y, v.y, ss); ss = fmaf(v.z, v.z, ss); ss = fmaf(v.w, v.w, ss);
+      }
+    }
+  };
+
+  stage(0, 0);
+  if (nk > 1) stage(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds();
+    if (kt + 2 < nk) stage((kt + 2) % S, kt + 2);
+    compute(kt % S);
+  }
+  barrier_lds();                                                // stage buffers free: reuse for the partials
+  if constexpr (WK > 1) {
+    if (wk > 0) {
+      float* dst = lds + ((wk - 1) * (NW / WK) + wr) * 64 * TI * TJ * 16;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            *reinterpret_cast<f32x4*>(dst + (((i * TJ + j) * 4 + r4) * 64 + lane) * 4) =
+                f32x4{acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]};
+      if (RS) ssr[((wk - 1) * (NW / WK) + wr) * 64 + lane] = ss;
+    }
+    barrier_lds();
+    if (wk == 0) {
+#pragma unroll
+      for (int g = 1; g < WK; ++g) {
+        const float* src = lds + ((g - 1) * (NW / WK) + wr) * 64 * TI * TJ * 16;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+              const f32x4 v = *reinterpret_cast<const f32x4*>(src + (((i * TJ + j) * 4 + r4) * 64 + lane) * 4);
+              acc[i][j][4 * r4] += v.x; acc[i][j][4 * r4 + 1] += v.y; acc[i][j][4 * r4 + 2] += v.z; acc[i][j][4 * r4 + 3] += v.w;
+            }
+        if (RS) ss += ssr[((g - 1) * (NW / WK) + wr) * 64 + lane];
+      }
+    }
+  }
+  if constexpr (RS) {
+    const float t = ss + __shfl_xor(ss, 32, 64);
+    if (wk == 0 && wn < TJ && lh == 0) rden[wm * WTM + 32 * jss + lr] = sqrtf(t) * p.inv_sqrt_k + kRmsEps;
+    barrier_lds();
+  }
+  if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
+}
+
 int num_cus_t() {
   static int n = 0;
   if (!n) {
@@ -473,6 +624,41 @@ hipError_t launch_t2_epi(const GemmArgs& a, int epi, hipStream_t st) {
     case EPI_RESID: return a.c_bf16 ? hipErrorInvalidValue : launch_t2<TL, EPI_RESID>(a, st);
     case EPI_SWIGLU: return launch_t2<TL, EPI_SWIGLU>(a, st);
     case EPI_GLU: return launch_t2<TL, EPI_GLU>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <class TL, int EPI>
+hipError_t launch_f32t(const GemmArgs& a, hipStream_t st) {
+  if (a.N % TL::BNW || a.K % (32 * TL::WK) || a.rpg || a.M <= 0 || (a.ldc % 4) || (a.lda % 4)) return hipErrorInvalidValue;
+  const int tiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
+  const dim3 block(TL::WN * TL::WM * TL::WK * 64);
+  if (a.rowscale) hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, true>), dim3(tiles), block, 0, st, a);
+  else hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, false>), dim3(tiles), block, 0, st, a);
+  return hipGetLastError();
+}
+
+template <class TL>
+hipError_t launch_f32t_epi(const GemmArgs& a, int epi, hipStream_t st) {
+  if (a.a_bf16 || a.c_bf16) return hipErrorInvalidValue;
+  constexpr bool pairable = (TL::BNW / TL::WN / 32) % 2 == 0;   // g/u 32-row blocks in one wave tile
+  switch (epi) {
+    case EPI_STORE: return launch_f32t<TL, EPI_STORE>(a, st);
+    case EPI_RESID: return launch_f32t<TL, EPI_RESID>(a, st);
+    case EPI_SWIGLU: if constexpr (pairable) return launch_f32t<TL, EPI_SWIGLU>(a, st); else return hipErrorInvalidValue;
+    case EPI_GLU: if constexpr (pairable) return launch_f32t<TL, EPI_GLU>(a, st); else return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// fp32 variants: 0 = 64x64 tile, 8 waves (2n x 2m x 2k); 1 = 128x64 (paired epilogues), 8 waves;
+// 2 = 64x64, 4 waves (no K split); 3 = 64x128 (2n x 2m x 2k, 32x64 wave tiles)
+hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st) {
+  switch (variant) {
+    case 0: return launch_f32t_epi<FT<64, 64, 2, 2, 2>>(a, epi, st);
+    case 1: return launch_f32t_epi<FT<128, 64, 2, 2, 2>>(a, epi, st);
+    case 2: return launch_f32t_epi<FT<64, 64, 2, 2, 1>>(a, epi, st);
+    case 3: return launch_f32t_epi<FT<64, 128, 2, 2, 2>>(a, epi, st);
     default: return hipErrorInvalidValue;
   }
 }

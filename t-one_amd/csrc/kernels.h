@@ -45,6 +45,8 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // persistent transposed-orientation bf16 GEMM (gemm_t.hip); variant = tile shape, see there
 hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
+// exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
+hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 
 // a3 conv2 as an implicit GEMM over all streams: A rows gathered from the channels-last
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,

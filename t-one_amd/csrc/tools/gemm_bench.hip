@@ -86,6 +86,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ref, (size_t)M * nout * 4)); CK(hipMalloc(&err, 4));
   const int64_t ws_cap = (int64_t)16 * M * N;
   CK(hipMalloc(&ws, ws_cap * 4));
+  float* ws_ss;
+  CK(hipMalloc(&ws_ss, (size_t)16 * M * 4));   // split-K row sums of squares (rowscale)
   // fp32 copies of the same (bf16-representable) operands for the fp32 path (variant -2)
   float *Af, *Wf;
   {
@@ -106,7 +108,7 @@ int main(int argc, char** argv) {
 
   GemmArgs a{};
   a.A = A; a.lda = K; a.W = W; a.C = C; a.ldc = nout; a.bias = bias; a.R = R; a.ldr = N; a.alpha = 1.f;
-  a.M = M; a.N = N; a.K = K; a.ws = ws; a.ws_cap = ws_cap; a.a_bf16 = 1; a.c_bf16 = cbf;
+  a.M = M; a.N = N; a.K = K; a.ws = ws; a.ws_ss = ws_ss; a.ws_cap = ws_cap; a.a_bf16 = 1; a.c_bf16 = cbf;
   a.C2 = epi == 1 ? C2 : nullptr;
   a.rowscale = rowscale;
   a.inv_sqrt_k = 1.0f / sqrtf((float)K);
@@ -125,13 +127,16 @@ int main(int argc, char** argv) {
     a.dbg = (fl >> 2) & 7;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
-    const bool f32 = (vv == -2);
+    const bool f32 = (vv == -2) || (v >= 30 && v < 40);
     a.A = f32 ? (const void*)Af : (const void*)A;
     a.W = f32 ? (const void*)Wf : (const void*)W;
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
-      return v < 0 ? gemm(a, epi, !f32, 0) : v >= 20 ? gemm_t(a, epi, v - 20, 0) : gemm_bf16_variant(a, epi, v, nsplit, 0);
+      return v < 0 ? gemm(a, epi, !f32, 0)
+             : v >= 30 ? gemm_f32t(a, epi, v - 30, 0)
+             : v >= 20 ? gemm_t(a, epi, v - 20, 0)
+                       : gemm_bf16_variant(a, epi, v, nsplit, 0);
     };
     hipError_t rc = launch();
     if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", v, hipGetErrorString(rc)); continue; }
