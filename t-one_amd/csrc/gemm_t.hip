@@ -23,6 +23,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace tone {
 namespace {
 
@@ -149,6 +151,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[T
             const f32x4 o = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
             if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
           }
+          if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);   // bf16 shadow (fp32 C)
         }
       }
     }
@@ -431,12 +434,15 @@ struct FT {
   static constexpr int BNW = BNW_, BMX = BMX_, WN = WN_, WM = WM_, WK = WK_;
 };
 
-template <class TL, int EPI, bool RS>
+template <class TL, int EPI, bool RS, bool BF>
 __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kernel(GemmArgs p) {
   constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, WK = TL::WK;
   constexpr int NW = WN * WM * WK, NT = NW * 64, S = 3;
   constexpr int WTN = BNW / WN, WTM = BMX / WM, TI = WTN / 32, TJ = WTM / 32;
-  constexpr int GROUP = (BNW + BMX) * 32;                       // floats of one k-group's slice
+  using E = typename std::conditional<BF, uint16_t, float>::type;   // operand element (bf16 bits / fp32)
+  constexpr int EPR = 128 / (int)sizeof(E);                     // elements per 128-byte row slice = K per group
+  constexpr int EPS = 16 / (int)sizeof(E);                      // elements per 16-byte slot
+  constexpr int GROUP = (BNW + BMX) * 32;                       // floats (= 128-byte rows) of one k-group's slice
   constexpr int STAGE = WK * GROUP;
   constexpr int PIECES = WK * (BNW + BMX) / 8, IPW = PIECES / NW;  // 1 KiB DMA instructions
   static_assert(PIECES % NW == 0 && IPW >= 1, "DMA pieces per wave");
@@ -458,9 +464,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kerne
     wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
   }
   const int m0 = (wgid / ntn) * BMX, n0 = (wgid % ntn) * BNW;
-  const int nk = p.K / (32 * WK);
-  const float* __restrict__ X = static_cast<const float*>(p.A);
-  const float* __restrict__ W = static_cast<const float*>(p.W);
+  const int nk = p.K / (EPR * WK);
+  const E* __restrict__ X = static_cast<const E*>(p.A);
+  const E* __restrict__ W = static_cast<const E*>(p.W);
 
   for (int i = tid; i < BNW; i += NT) sbias[i] = p.bias ? p.bias[n0 + i] : 0.f;
   __syncthreads();
@@ -473,9 +479,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kerne
       const int piece = wid + i * NW;                           // 8 rows x 128 B
       const int g = piece / ((BNW + BMX) / 8), pr = piece % ((BNW + BMX) / 8);
       const int row = pr * 8 + (lane >> 3);                     // row of [W rows | X rows]
-      const int k0 = (kt * WK + g) * 32 + (((lane & 7) ^ ((row >> 1) & 7)) << 2);
-      const float* src = row < BNW ? W + (int64_t)(n0 + row) * p.K + k0
-                                   : X + (int64_t)min(m0 + row - BNW, p.M - 1) * p.lda + k0;
+      const int k0 = (kt * WK + g) * EPR + ((lane & 7) ^ ((row >> 1) & 7)) * EPS;
+      const E* src = row < BNW ? W + (int64_t)(n0 + row) * p.K + k0
+                               : X + (int64_t)min(m0 + row - BNW, p.M - 1) * p.lda + k0;
 #if defined(__HIP_DEVICE_COMPILE__)
       __builtin_amdgcn_global_load_lds(src, base + g * GROUP + pr * 8 * 32, 16, 0, 0);
 #else
@@ -495,26 +501,44 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kerne
   const int jss = wn % TJ;                                      // m-tile whose sum of squares this wave keeps
 
   auto compute = [&](int buf) {
-    const float* base = lds + buf * STAGE + wk * GROUP;
+    const float* base = lds + buf * STAGE + wk * GROUP;         // rows of 32 floats = 128 bytes
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int off = ((2 * q + lh) ^ cs) << 2;
-      f32x4 fa[TI], fb[TJ];
+      const int off = ((2 * q + lh) ^ cs) << 2;                 // float offset of the 16-byte slot
+      if constexpr (BF) {
+        bf16x8 fa[TI], fb[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) fa[i] = *reinterpret_cast<const f32x4*>(base + (wn * WTN + 32 * i + lr) * 32 + off);
+        for (int i = 0; i < TI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(base + (wn * WTN + 32 * i + lr) * 32 + off);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) fb[j] = *reinterpret_cast<const f32x4*>(base + (BNW + wm * WTM + 32 * j + lr) * 32 + off);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
+        for (int j = 0; j < TJ; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(base + (BNW + wm * WTM + 32 * j + lr) * 32 + off);
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][e], fb[j][e], acc[i][j], 0, 0, 0);
-      if constexpr (RS) {
-        f32x4 v = fb[0];
+          for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        if constexpr (RS) {
+          bf16x8 v = fb[0];
 #pragma unroll
-        for (int j = 1; j < TJ; ++j) v = (jss == j) ? fb[j] : v;
-        ss = fmaf(v.x, v.x, ss); ss = fmaf(v.y, v.y, ss); ss = fmaf(v.z, v.z, ss); ss = fmaf(v.w, v.w, ss);
+          for (int j = 1; j < TJ; ++j) v = (jss == j) ? fb[j] : v;
+          ss = sumsq8(v, ss);
+        }
+      } else {
+        f32x4 fa[TI], fb[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) fa[i] = *reinterpret_cast<const f32x4*>(base + (wn * WTN + 32 * i + lr) * 32 + off);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) fb[j] = *reinterpret_cast<const f32x4*>(base + (BNW + wm * WTM + 32 * j + lr) * 32 + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][e], fb[j][e], acc[i][j], 0, 0, 0);
+        if constexpr (RS) {
+          f32x4 v = fb[0];
+#pragma unroll
+          for (int j = 1; j < TJ; ++j) v = (jss == j) ? fb[j] : v;
+          ss = fmaf(v.x, v.x, ss); ss = fmaf(v.y, v.y, ss); ss = fmaf(v.z, v.z, ss); ss = fmaf(v.w, v.w, ss);
+        }
       }
     }
   };
@@ -628,19 +652,27 @@ hipError_t launch_t2_epi(const GemmArgs& a, int epi, hipStream_t st) {
   }
 }
 
-template <class TL, int EPI>
+template <class TL, int EPI, bool BF>
 hipError_t launch_f32t(const GemmArgs& a, hipStream_t st) {
-  if (a.N % TL::BNW || a.K % (32 * TL::WK) || a.rpg || a.M <= 0 || (a.ldc % 4) || (a.lda % 4)) return hipErrorInvalidValue;
+  const int kg = BF ? 64 : 32;
+  if (a.N % TL::BNW || a.K % (kg * TL::WK) || a.rpg || a.M <= 0 || (a.ldc % 8) || (a.lda % 8)) return hipErrorInvalidValue;
   const int tiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
-  if (a.rowscale) hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, true>), dim3(tiles), block, 0, st, a);
-  else hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, false>), dim3(tiles), block, 0, st, a);
+  if (a.rowscale) hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, true, BF>), dim3(tiles), block, 0, st, a);
+  else hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, false, BF>), dim3(tiles), block, 0, st, a);
   return hipGetLastError();
+}
+
+template <class TL, int EPI>
+hipError_t launch_f32t(const GemmArgs& a, hipStream_t st) {
+  if (a.a_bf16) return launch_f32t<TL, EPI, true>(a, st);
+  if (a.c_bf16) return hipErrorInvalidValue;
+  return launch_f32t<TL, EPI, false>(a, st);
 }
 
 template <class TL>
 hipError_t launch_f32t_epi(const GemmArgs& a, int epi, hipStream_t st) {
-  if (a.a_bf16 || a.c_bf16) return hipErrorInvalidValue;
+  if (epi == EPI_RESID && a.c_bf16) return hipErrorInvalidValue;
   constexpr bool pairable = (TL::BNW / TL::WN / 32) % 2 == 0;   // g/u 32-row blocks in one wave tile
   switch (epi) {
     case EPI_STORE: return launch_f32t<TL, EPI_STORE>(a, st);

@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
   GemmArgs a{};
   a.A = A; a.lda = K; a.W = W; a.C = C; a.ldc = nout; a.bias = bias; a.R = R; a.ldr = N; a.alpha = 1.f;
   a.M = M; a.N = N; a.K = K; a.ws = ws; a.ws_ss = ws_ss; a.ws_cap = ws_cap; a.a_bf16 = 1; a.c_bf16 = cbf;
-  a.C2 = epi == 1 ? C2 : nullptr;
+  a.C2 = (epi == 1 || (epi == 0 && !cbf)) ? C2 : nullptr;   // the session's shadowed outputs
   a.rowscale = rowscale;
   a.inv_sqrt_k = 1.0f / sqrtf((float)K);
   hipEvent_t e0, e1;
@@ -134,6 +134,7 @@ int main(int argc, char** argv) {
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
       return v < 0 ? gemm(a, epi, !f32, 0)
+             : v >= 40 ? gemm_f32t(a, epi, v - 40, 0)
              : v >= 30 ? gemm_f32t(a, epi, v - 30, 0)
              : v >= 20 ? gemm_t(a, epi, v - 20, 0)
                        : gemm_bf16_variant(a, epi, v, nsplit, 0);
@@ -143,8 +144,13 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     CK(hipMemset(err, 0, 4));
     hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, a.c_bf16, ref, (int64_t)M * nout, err);
-    float herr;
+    float herr, herr2 = 0.f;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+    if (a.C2) {   // the bf16 shadow must hold the same values (bf16-rounded)
+      CK(hipMemset(err, 0, 4));
+      hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)a.C2, 1, ref, (int64_t)M * nout, err);
+      CK(hipMemcpy(&herr2, err, 4, hipMemcpyDeviceToHost));
+    }
     for (int i = 0; i < 3; ++i) CK(launch());
     CK(hipEventRecord(e0, 0));
     for (int i = 0; i < iters; ++i) CK(launch());
@@ -153,8 +159,8 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
-    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g}\n",
-           M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr);
+    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"shadow_err\": %.3g}\n",
+           M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr, herr2);
     fflush(stdout);
   }
   return 0;
