@@ -57,6 +57,33 @@ def family_flops_per_stream() -> dict:
     return f
 
 
+def measured_traffic(family: str, precision: str, batch: int):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (scripts/pmc_traffic.sh + scripts/traffic_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950
+    correction), or (None, None) when no summary exists for this precision / batch."""
+    path = os.path.join(ROOT, "profiles", f"r01_traffic_{precision}_b{batch}.json")
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("kernel") != family:
+        return None, None
+    return int(t["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+
+
+def algo_bytes(family: str, precision: str, batch: int) -> float:
+    """Algorithmic HBM bytes per launch of a GEMM family: A read + W read + C write, averaged over the
+    family's launches in one step (only the FFN up-projection is modelled)."""
+    if family != "gemm_ffn_up":
+        return 0.0
+    e = 4 if precision == "fp32" else 2
+    d, ff = C.D_MODEL, C.D_FF
+    per = [e * (batch * C.layer_frames(l) * d + 2 * ff * d + batch * C.layer_frames(l) * ff)
+           for l in range(C.N_LAYERS) for _ in range(2)]
+    return sum(per) / len(per)
+
+
 def synthetic_pcm(rng, b, n_chunks, silence=0.2):
     """Gaussian sigma=3000 clipped to int16, 20 % silent chunks."""
     x = np.clip(np.round(rng.normal(0.0, 3000.0, size=(n_chunks, b, C.AUDIO_CHUNK_SAMPLES))), -32768, 32767)
@@ -153,8 +180,10 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True)
         f = fams[dom]
         achieved = f["flop_per_launch"] / (f["avg_us"] * 1e-6) / 1e12
         peak = PEAK_TFLOPS[precision]
+        traffic, tsrc = measured_traffic(dom, precision, B)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": tsrc, "algo_bytes": int(algo_bytes(dom, precision, B)),
                 "avg_us": round(f["avg_us"], 2), "flop_per_launch": int(f["flop_per_launch"]),
                 "step_tflops": round(C.FLOP_PER_CHUNK * B / (elapsed / args.steps) / 1e12, 2),
                 "families_us_per_step": {k: round(v["avg_us"] * v["launches_per_step"], 1) for k, v in fams.items()}}

@@ -1,0 +1,27 @@
+"""Per-launch HBM traffic of the FFN up-projection launches from the PMC passes of
+scripts/pmc_traffic.sh.  FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the
+bytes of wide streaming reads (MI355X_MICROARCH.md, HBM), so fetch bytes = 2 x FETCH_SIZE x 1024.
+The FFN up-projection is the only GEMM with the SWIGLU epilogue; its kernels are recognised by name.
+Usage: python scripts/traffic_summary.py gpurun_out/pmc_<prec> <prec> <batch> > profiles/<file>.json"""
+import csv, glob, json, re, sys
+
+root, prec, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
+PAT = {  # SWIGLU instantiations: EPI_SWIGLU = 2
+    "fp32": re.compile(r"gemm_kernel<tone::Tile<\d+, \d+, \d+, \d+>, 2,"),
+    "bf16": re.compile(r"gemm_t_kernel<.*TT<\d+, \d+, \d+, \d+>, 2, (true|false)>"),
+}[prec]
+
+
+def per_launch(sub):
+    f = glob.glob(f"{root}/{sub}/**/*counter_collection.csv", recursive=True)[0]
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if PAT.search(r["Kernel_Name"])]
+    return vals
+
+
+fetch, write = per_launch("fetch"), per_launch("write")
+fb = 2 * 1024 * sum(fetch) / len(fetch)
+wb = 1024 * sum(write) / len(write)
+print(json.dumps({"kernel": "gemm_ffn_up", "precision": prec, "batch": batch, "launches_fetch": len(fetch),
+                  "launches_write": len(write), "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
+                  "traffic_bytes_per_launch": round(fb + wb),
+                  "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes, eager launches; fetch x2 (gfx950)"}))
