@@ -50,27 +50,31 @@ constexpr int kK1 = kSub1Kt * kSub1Kf;      // 231
 constexpr int kK1P = 256;                   // padded K
 constexpr int kPos1 = kMelT * kSub1F;       // 1320
 
-template <bool OBF>   // x2 stored as bf16 bits (bf16 mode) or fp32
-__global__ void __launch_bounds__(256) sub1_kernel(const float* __restrict__ feats, StateRef s,
-                                                   const float* __restrict__ pre_norm_w, const float* __restrict__ w1,
-                                                   const float* __restrict__ scale1, const float* __restrict__ shift1,
-                                                   void* __restrict__ x2) {
-  using XT = typename std::conditional<OBF, __bf16, float>::type;
-  __shared__ float x1[(kSub1S + kMelT) * kMels];
-  __shared__ float wk[kSub1C][kK1P + 1];
-  __shared__ int koff[kK1P];
+// ---- fp32 (exact-fp32 MFMA v_mfma_f32_32x32x2_f32): 8 waves per stream, 32-position tiles; the tap
+// loop runs kt (11) x kf pairs (11, the 22nd tap zero-weighted), so the gathered x1 address is plain
+// arithmetic (no tap table).
+constexpr int kKfP = 22;                    // kf padded to an even count (fp32 path)
+
+__global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__ feats, StateRef s,
+                                                       const float* __restrict__ pre_norm_w,
+                                                       const float* __restrict__ w1, const float* __restrict__ scale1,
+                                                       const float* __restrict__ shift1, float* __restrict__ x2) {
+  __shared__ float x1[(kSub1S + kMelT) * kMels + 32];   // +32: taps past column 63 read zeros
+  __shared__ float wk[kSub1C][kSub1Kt * kKfP + 1];
   __shared__ float sc[kSub1C], sh[kSub1C];
+  __shared__ __half st2[kSub1C * kSub2S * kSub1F];      // sub2 state [c][8][44]: carried in, then next
+  __shared__ __attribute__((aligned(16))) float tbuf[8][32 * kSub1C];   // per-wave output tile (32 pos x 32 ch)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t srow = s.row(b);
-  for (int i = tid; i < kSub1C * kK1P; i += 256) {
-    const int c = i / kK1P, k = i % kK1P;
-    wk[c][k] = k < kK1 ? w1[c * kK1 + k] : 0.f;
+  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) st2[i] = s.in[srow + kOffSub2 + i];
+  for (int i = tid; i < kSub1C * kSub1Kt * kKfP; i += 512) {
+    const int c = i / (kSub1Kt * kKfP), k = i % (kSub1Kt * kKfP), kt = k / kKfP, kf = k % kKfP;
+    wk[c][k] = kf < kSub1Kf ? w1[(c * kSub1Kt + kt) * kSub1Kf + kf] : 0.f;
   }
-  for (int k = tid; k < kK1P; k += 256) koff[k] = k < kK1 ? (k / kSub1Kf) * kMels + k % kSub1Kf : 0;
   if (tid < kSub1C) { sc[tid] = scale1[tid]; sh[tid] = shift1[tid]; }
-  for (int i = tid; i < kSub1S * kMels; i += 256) x1[i] = __half2float(s.in[srow + kOffSub1 + i]);
-  // RMSNorm over 64 features: one wave per frame, one lane per feature
-  for (int t = wid; t < kMelT; t += 4) {
+  for (int i = tid; i < kSub1S * kMels; i += 512) x1[i] = __half2float(s.in[srow + kOffSub1 + i]);
+  if (tid < 32) x1[(kSub1S + kMelT) * kMels + tid] = 0.f;
+  for (int t = wid; t < kMelT; t += 8) {   // RMSNorm over 64 features: one wave per frame
     const float v = feats[((int64_t)b * kMelT + t) * kMels + lane];
     const float ssq = wave_sum(v * v);
     const float rms = sqrtf(ssq) * 0.125f;          // * 64^-0.5
@@ -78,58 +82,172 @@ __global__ void __launch_bounds__(256) sub1_kernel(const float* __restrict__ fea
     x1[(kSub1S + t) * kMels + lane] = y;
     if (t >= kMelT - kSub1S) s.out[srow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
   }
-  // carried conv2 input rows -> x2 rows 0..7 (channels-last)
-  XT* xb = static_cast<XT*>(x2) + (int64_t)b * kSub2In * kSub1F * kSub1C;
-  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 256) {
-    const int c = i / (kSub2S * kSub1F), r = (i / kSub1F) % kSub2S, f = i % kSub1F;
-    xb[(r * kSub1F + f) * kSub1C + c] = (XT)__half2float(s.in[srow + kOffSub2 + i]);
-  }
+  float* xb = x2 + (int64_t)b * kSub2In * kSub1F * kSub1C;
   __syncthreads();
+  for (int i = tid; i < kSub1C * kSub2S * kSub1F / 4; i += 512) {   // carried rows -> x2 rows 0..7 (channels-last)
+    const int c = (4 * i) % kSub1C, rf = (4 * i) / kSub1C;            // 4 channels per thread, 16-byte stores
+    const int e = c * kSub2S * kSub1F + rf;
+    *reinterpret_cast<float4*>(xb + 4 * i) =
+        make_float4(__half2float(st2[e]), __half2float(st2[e + kSub2S * kSub1F]), __half2float(st2[e + 2 * kSub2S * kSub1F]),
+                    __half2float(st2[e + 3 * kSub2S * kSub1F]));
+  }
+  __syncthreads();                                              // st2 is reused for the next state below
   const int li = lane & 31, lh = lane >> 5;
-  for (int tile = wid; tile * 32 < kPos1; tile += 4) {
+  for (int tile = wid; tile * 32 < kPos1; tile += 8) {
     const int pos = min(tile * 32 + li, kPos1 - 1);
-    const int base = (pos / kSub1F) * kMels + pos % kSub1F;
+    const float* xa = x1 + (pos / kSub1F) * kMels + pos % kSub1F + lh;
+    const float* wb = &wk[li][lh];
     f32x16_t acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if constexpr (OBF) {
-      // bf16 mode: v_mfma_f32_32x32x16_bf16, lane (i, h) holds A[pos_i][16s + 8h + e] (gathered)
-#pragma unroll 4
-      for (int st = 0; st < kK1P / 16; ++st) {
-        bf16x8_t av, bv;
+    for (int kt = 0; kt < kSub1Kt; ++kt) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int k = 16 * st + 8 * lh + e;
-          av[e] = (__bf16)x1[base + koff[k]];
-          bv[e] = (__bf16)wk[li][k];
-        }
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
-      }
-    } else {
-#pragma unroll 8
-      for (int st = 0; st < kK1P / 2; ++st) {
-        const int k = 2 * st + lh;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[base + koff[k]], wk[li][k], acc, 0, 0, 0);
-      }
+      for (int k2 = 0; k2 < kKfP / 2; ++k2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[kt * kMels + 2 * k2], wb[kt * kKfP + 2 * k2], acc, 0, 0, 0);
     }
     const int c = li;
+    float* tw = tbuf[wid];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int p = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int pl = (r & 3) + 8 * (r >> 2) + 4 * lh, p = tile * 32 + pl;
+      const float y = silu_f(fmaf(acc[r], sc[c], sh[c]));
+      tw[pl * kSub1C + c] = y;
       if (p >= kPos1) continue;
       const int t = p / kSub1F, f = p % kSub1F;
-      const float y = silu_f(fmaf(acc[r], sc[c], sh[c]));
-      xb[((kSub2S + t) * kSub1F + f) * kSub1C + c] = (XT)y;
-      if (t >= kMelT - kSub2S)
-        s.out[srow + kOffSub2 + (c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
+      if (t >= kMelT - kSub2S) st2[(c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the tile's 32 positions are consecutive in the flattened (t, f) order: one contiguous 4 KB run
+    float* dst = xb + (int64_t)(kSub2S * kSub1F + tile * 32) * kSub1C;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int v = lane + 64 * q, pl = v >> 3;
+      if (tile * 32 + pl < kPos1) *reinterpret_cast<float4*>(dst + v * 4) = *reinterpret_cast<const float4*>(tw + v * 4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
+  __syncthreads();
+  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) s.out[srow + kOffSub2 + i] = st2[i];
 }
 
-hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const float* scale1,
-                       const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st) {
-  if (x2_bf16) hipLaunchKernelGGL(sub1_kernel<true>, dim3(B), dim3(256), 0, st, feats, s, pre_norm_w, w1, scale1, shift1, x2);
-  else hipLaunchKernelGGL(sub1_kernel<false>, dim3(B), dim3(256), 0, st, feats, s, pre_norm_w, w1, scale1, shift1, x2);
+// ---- bf16 (v_mfma_f32_16x16x32_bf16): conv1 as a Toeplitz GEMM.  For output row t and kernel row
+// kt the 21 kf taps are padded to 32, so one MFMA's K = one kernel row; lane (position f, group g)
+// needs x1[t + kt][f + 8g .. f + 8g + 7], which is 16-byte aligned in one of 8 shifted bf16 copies of
+// x1 kept in LDS (copy s holds row[j + s]).  The weights ([kt][c][32] bf16, 22 fragments) stay in
+// registers for the whole workgroup.  Tiles: 16 positions (f0 = 0, 16, 32 of one row t) x 32
+// channels (2 MFMA column tiles); 90 tiles per stream over 8 waves.
+constexpr int kX1Cols = 80;                 // shifted-copy row length (taps reach column 43 + 31)
+
+__global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict__ feats, StateRef s,
+                                                        const float* __restrict__ pre_norm_w,
+                                                        const uint16_t* __restrict__ w1t, const float* __restrict__ scale1,
+                                                        const float* __restrict__ shift1, uint16_t* __restrict__ x2) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int kRows = kSub1S + kMelT;     // 40
+  // 8 shifted copies, each padded by 32 B so the copies start 8 banks apart (a wave's A reads hit
+  // all 8 copies at the same in-copy offset)
+  constexpr int kCopy = kRows * kX1Cols + 16;
+  __shared__ __attribute__((aligned(16))) uint16_t xc[8 * kCopy];
+  __shared__ float x1[kRows * kMels];
+  __shared__ float sc[kSub1C], sh[kSub1C];
+  __shared__ __half st2[kSub1C * kSub2S * kSub1F];      // sub2 state [c][8][44]: carried in, then next
+  __shared__ __attribute__((aligned(16))) uint16_t tbuf[8][16 * kSub1C];   // per-wave output tile (16 pos x 32 ch)
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t srow = s.row(b);
+  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) st2[i] = s.in[srow + kOffSub2 + i];
+  // weight fragments: B operand lane (n = lane & 15, k group g = lane >> 4): w1t[kt][16 nt + n][8 g .. 8 g + 7]
+  const int g = lane >> 4, n = lane & 15;
+  bf16x8 wf[kSub1Kt][2];
+#pragma unroll
+  for (int kt = 0; kt < kSub1Kt; ++kt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      wf[kt][nt] = *reinterpret_cast<const bf16x8*>(w1t + ((kt * kSub1C + 16 * nt + n) * 32 + 8 * g));
+  if (tid < kSub1C) { sc[tid] = scale1[tid]; sh[tid] = shift1[tid]; }
+  for (int i = tid; i < kSub1S * kMels; i += 512) x1[i] = __half2float(s.in[srow + kOffSub1 + i]);
+  for (int t = wid; t < kMelT; t += 8) {
+    const float v = feats[((int64_t)b * kMelT + t) * kMels + lane];
+    const float ssq = wave_sum(v * v);
+    const float rms = sqrtf(ssq) * 0.125f;
+    const float y = pre_norm_w[lane] * (v / (rms + kRmsEps));
+    x1[(kSub1S + t) * kMels + lane] = y;
+    if (t >= kMelT - kSub1S) s.out[srow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
+  }
+  uint16_t* xb = x2 + (int64_t)b * kSub2In * kSub1F * kSub1C;
+  __syncthreads();
+  for (int i = tid; i < kSub1C * kSub2S * kSub1F / 8; i += 512) {   // carried rows -> x2 rows 0..7 (channels-last)
+    const int c = (8 * i) % kSub1C, rf = (8 * i) / kSub1C;            // 8 channels per thread, 16-byte stores
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const __bf16 lo = (__bf16)__half2float(st2[(c + 2 * q) * kSub2S * kSub1F + rf]);
+      const __bf16 hi = (__bf16)__half2float(st2[(c + 2 * q + 1) * kSub2S * kSub1F + rf]);
+      w[q] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+    *reinterpret_cast<uint4*>(xb + 8 * i) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  for (int i = tid; i < 8 * kRows * kX1Cols; i += 512) {   // shifted bf16 copies
+    const int sh8 = i / (kRows * kX1Cols), r = (i / kX1Cols) % kRows, j = i % kX1Cols;
+    const float v = (j + sh8 < kMels) ? x1[r * kMels + j + sh8] : 0.f;
+    const __bf16 h = (__bf16)v;
+    xc[sh8 * kCopy + r * kX1Cols + j] = __builtin_bit_cast(uint16_t, h);
+  }
+  __syncthreads();
+  for (int tile = wid; tile < kMelT * 3; tile += 8) {
+    const int t = tile / 3, f0 = (tile % 3) * 16;
+    const int a = f0 + n + 8 * g, sh8 = a & 7;                 // A operand: position f0 + n, k group g
+    const uint16_t* arow = xc + sh8 * kCopy + t * kX1Cols + (a - sh8);
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kt = 0; kt < kSub1Kt; ++kt) {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(arow + kt * kX1Cols);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wf[kt][0], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wf[kt][1], acc[1], 0, 0, 0);
+    }
+    // D layout 16x16: lane holds column (channel) n + 16 nt, rows (positions) f0 + 4 g + r; the tile
+    // goes through the wave's LDS slice so the 16 positions x 64 B (contiguous in x2) leave as one
+    // 16-byte store per lane
+    uint16_t* tw = tbuf[wid];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int c = 16 * nt + n;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = f0 + 4 * g + r;
+        const float z = fmaf(acc[nt][r], sc[c], sh[c]);   // SiLU via v_exp_f32 / v_rcp_f32 (bf16 output)
+        const float y = z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
+        const __bf16 hy = (__bf16)y;
+        tw[(4 * g + r) * kSub1C + c] = __builtin_bit_cast(uint16_t, hy);
+        if (f < kSub1F && t >= kMelT - kSub2S) st2[(c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (f0 + (lane >> 2) < kSub1F)
+      *reinterpret_cast<uint4*>(xb + ((int64_t)(kSub2S + t) * kSub1F + f0) * kSub1C + lane * 8) =
+          *reinterpret_cast<const uint4*>(tw + lane * 8);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) s.out[srow + kOffSub2 + i] = st2[i];
+}
+
+hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
+                       const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st) {
+  if (x2_bf16) {
+    if (!w1t) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sub1_bf16_kernel, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w,
+                       static_cast<const uint16_t*>(w1t), scale1, shift1, static_cast<uint16_t*>(x2));
+  } else {
+    hipLaunchKernelGGL(sub1_f32_kernel, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w, w1, scale1, shift1,
+                       static_cast<float*>(x2));
+  }
   return hipGetLastError();
 }
 

@@ -109,7 +109,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[T
           const int n = nl + (r & 3) + 8 * (r >> 2) + 4 * lh;
           const float g = fmaf(acc[2 * ip][j][r], inv, sb[n]);
           const float u = fmaf(acc[2 * ip + 1][j][r], inv, sb[n + 32]);
-          o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
+          if (p.c_bf16) o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
+          else o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);   // fp32 output: IEEE exp/div
         }
         if (p.c_bf16) {
           store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, o, lh, ok);
@@ -592,6 +593,259 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kerne
   if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 projections on the bf16 MFMA by exact operand splitting ("x3": three bf16 terms per fp32
+// value, six cross products).
+//
+//   x = x0 + x1 + x2,  x0 = bf16_rn(x), x1 = bf16_rn(x - x0), x2 = bf16_rn(x - x0 - x1)
+//
+// Both residuals are exact in fp32 and three 8-bit significands cover fp32's 24:
+// |x - x0 - x1 - x2| <= 2^-27 |x|.  A bf16 x bf16 product is exact in the MFMA's fp32 accumulator,
+// so keeping the six products with i + j <= 2,
+//
+//   W.X = W0.X0 + W0.X1 + W1.X0 + W0.X2 + W1.X1 + W2.X0   (dropped terms <= 3 * 2^-26 |W||X|),
+//
+// is an fp32-accurate dot product (tests/test_gpu_parity.py::test_fp32_split_vs_fp32_mfma runs the
+// whole step both ways against the oracle; tools/gemm_bench with FULLF32=1 compares both GEMMs
+// with an fp64 reference).  Cost: 6 x 32 cycles per 32x32x16 step on v_mfma_f32_32x32x16_bf16
+// against 8 x 64 on v_mfma_f32_32x32x2_f32 -- 2.67x the fp32 MFMA rate.
+// W is constant: split once at upload into three bf16 planes [3][N][K] (session.hip upload_w).
+// X stays fp32 in memory (its producers are unchanged) and is split in registers from its LDS
+// fragment, 8 values per lane per 16-deep k-step, the VALU issued between the MFMAs.
+// Structure as gemm_f32t_kernel above (transposed orientation, shared epilogue, in-workgroup K
+// split over WK wave groups, LDS-DMA ring of S stages).  Per wave group and K-step (32 k) a stage
+// holds the three W planes (BNW rows x 64 B each, 16-byte slot ^= (row >> 2) & 3) and X (BMX rows
+// x 128 B fp32, slot ^= (row >> 1) & 7); both swizzles go on the per-lane DMA source address and
+// are undone on the ds_read_b128.
+template <int BNW_, int BMX_, int WN_, int WM_, int WK_, int S_>
+struct XT {
+  static constexpr int BNW = BNW_, BMX = BMX_, WN = WN_, WM = WM_, WK = WK_, S = S_;
+};
+
+// 8 fp32 values -> their three bf16 terms (round-to-nearest-even at each level)
+__device__ __forceinline__ void split3(const f32x4 a, const f32x4 b, bf16x8& h, bf16x8& m, bf16x8& l) {
+  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 x0 = (__bf16)x[e];
+    const float r1 = x[e] - (float)x0;
+    const __bf16 x1 = (__bf16)r1;
+    const float r2 = r1 - (float)x1;
+    h[e] = x0;
+    m[e] = x1;
+    l[e] = (__bf16)r2;
+  }
+}
+
+template <class TL, int EPI, bool RS>
+__global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(GemmArgs p) {
+  constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, WK = TL::WK, S = TL::S;
+  constexpr int NW = WN * WM * WK, NT = NW * 64;
+  constexpr int WTN = BNW / WN, WTM = BMX / WM, TI = WTN / 32, TJ = WTM / 32;
+  constexpr int WPL = BNW * 16;                                 // floats of one W plane slice (64-B rows)
+  constexpr int GROUP = 3 * WPL + BMX * 32;                     // floats of one wave group's slice
+  constexpr int STAGE = WK * GROUP;
+  constexpr int WPC = 3 * BNW / 16, XPC = BMX / 8;              // 1 KiB DMA pieces per group
+  constexpr int PIECES = WK * (WPC + XPC), IPW = PIECES / NW;
+  static_assert(PIECES % NW == 0 && IPW >= 1, "DMA pieces per wave");
+  static_assert(TI >= 1 && TJ >= 1 && WN >= TJ, "wave tile / row-scale ownership");
+  static_assert(S == 2 || S == 3, "2 or 3 LDS stages");
+  constexpr int RED = (WK - 1) * (NW / WK) * 64 * TI * TJ * 16;  // K-split partials (floats)
+  constexpr int LDSF = (S * STAGE > RED ? S * STAGE : RED);
+  // ONE LDS object (a second __shared__ array beside LDS-DMA staging can cost a vmcnt(0) per step)
+  __shared__ __attribute__((aligned(16))) float lds[LDSF + BNW + BMX + (WK - 1) * (NW / WK) * 64];
+  float* sbias = lds + LDSF;
+  float* rden = sbias + BNW;
+  float* ssr = rden + BMX;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wid / (WN * WM), wr = wid % (WN * WM), wn = wr / WM, wm = wr % WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int ntn = p.N / BNW;
+  int wgid = blockIdx.x;
+  {  // XCD-contiguous tile order (bijective for any grid size)
+    const int nwg = gridDim.x, xcd = wgid & 7, q = nwg >> 3, rr = nwg & 7;
+    wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
+  }
+  const int m0 = (wgid / ntn) * BMX, n0 = (wgid % ntn) * BNW;
+  const int nk = p.K / (32 * WK);
+  const float* __restrict__ X = static_cast<const float*>(p.A);
+  const uint16_t* __restrict__ W3 = p.W3;
+  const int64_t plane = (int64_t)p.N * p.K;
+
+  for (int i = tid; i < BNW; i += NT) sbias[i] = p.bias ? p.bias[n0 + i] : 0.f;
+  __syncthreads();
+
+  auto stage = [&](int buf, int kt) {
+    float* base = lds + buf * STAGE;
+    (void)base;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int piece = wid + i * NW;                           // wave-uniform
+      const int g = piece / (WPC + XPC), pr = piece % (WPC + XPC);
+      const int kb = (kt * WK + g) * 32;
+      const void* src;
+      float* dst;
+      if (pr < WPC) {                                           // 16 W rows x 64 B of plane pl
+        const int pl = pr / (BNW / 16), rb = (pr % (BNW / 16)) * 16, row = rb + (lane >> 2);
+        const int slot = (lane & 3) ^ ((row >> 2) & 3);
+        src = W3 + pl * plane + (int64_t)(n0 + row) * p.K + kb + slot * 8;
+        dst = base + g * GROUP + pl * WPL + rb * 16;
+      } else {                                                  // 8 X rows x 128 B
+        const int rb = (pr - WPC) * 8, row = rb + (lane >> 3);
+        const int slot = (lane & 7) ^ ((row >> 1) & 7);
+        src = X + (int64_t)min(m0 + row, p.M - 1) * p.lda + kb + slot * 4;
+        dst = base + g * GROUP + 3 * WPL + rb * 32;
+      }
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+#else
+      (void)src;
+      (void)dst;
+#endif
+    }
+  };
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float ss = 0.f;
+  const int jss = wn % TJ;                                      // m-tile whose sum of squares this wave keeps
+
+  auto compute = [&](int buf) {
+    const float* base = lds + buf * STAGE + wk * GROUP;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j8 = 2 * q + lh;                                // 8-value block of the 32-k slice
+      bf16x8 w[3][TI], xs[3][TJ];
+      f32x4 xv[TJ][2];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int row = wn * WTN + 32 * i + lr;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          w[pl][i] = *reinterpret_cast<const bf16x8*>(base + pl * WPL + row * 16 + ((j8 ^ ((row >> 2) & 3)) << 2));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int row = wm * WTM + 32 * j + lr, cs = (row >> 1) & 7;
+        const float* xr = base + 3 * WPL + row * 32;
+        xv[j][0] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8) ^ cs) << 2));
+        xv[j][1] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8 + 1) ^ cs) << 2));
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) split3(xv[j][0], xv[j][1], xs[0][j], xs[1][j], xs[2][j]);
+      if constexpr (RS) {
+        f32x4 a = xv[0][0], b = xv[0][1];
+#pragma unroll
+        for (int j = 1; j < TJ; ++j) {
+          a = (jss == j) ? xv[j][0] : a;
+          b = (jss == j) ? xv[j][1] : b;
+        }
+        ss = fmaf(a.x, a.x, ss); ss = fmaf(a.y, a.y, ss); ss = fmaf(a.z, a.z, ss); ss = fmaf(a.w, a.w, ss);
+        ss = fmaf(b.x, b.x, ss); ss = fmaf(b.y, b.y, ss); ss = fmaf(b.z, b.z, ss); ss = fmaf(b.w, b.w, ss);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {   // small terms first
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2][i], xs[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1][i], xs[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0][i], xs[2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1][i], xs[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0][i], xs[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0][i], xs[0][j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  if constexpr (S == 3) {
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds();                                            // buffer (kt+2)%3 was read in step kt-1
+      if (kt + 2 < nk) stage((kt + 2) % 3, kt + 2);
+      compute(kt % 3);
+    }
+  } else {
+    stage(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds();                                            // buffer (kt+1)&1 was read in step kt-1
+      if (kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
+      compute(kt & 1);
+    }
+  }
+  barrier_lds();                                                // stage buffers free: reuse for the partials
+  if constexpr (WK > 1) {
+    if (wk > 0) {
+      float* dst = lds + ((wk - 1) * (NW / WK) + wr) * 64 * TI * TJ * 16;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            *reinterpret_cast<f32x4*>(dst + (((i * TJ + j) * 4 + r4) * 64 + lane) * 4) =
+                f32x4{acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]};
+      if (RS) ssr[((wk - 1) * (NW / WK) + wr) * 64 + lane] = ss;
+    }
+    barrier_lds();
+    if (wk == 0) {
+#pragma unroll
+      for (int g = 1; g < WK; ++g) {
+        const float* src = lds + ((g - 1) * (NW / WK) + wr) * 64 * TI * TJ * 16;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+              const f32x4 v = *reinterpret_cast<const f32x4*>(src + (((i * TJ + j) * 4 + r4) * 64 + lane) * 4);
+              acc[i][j][4 * r4] += v.x; acc[i][j][4 * r4 + 1] += v.y; acc[i][j][4 * r4 + 2] += v.z; acc[i][j][4 * r4 + 3] += v.w;
+            }
+        if (RS) ss += ssr[((g - 1) * (NW / WK) + wr) * 64 + lane];
+      }
+    }
+  }
+  if constexpr (RS) {
+    const float t = ss + __shfl_xor(ss, 32, 64);
+    if (wk == 0 && wn < TJ && lh == 0) rden[wm * WTM + 32 * jss + lr] = sqrtf(t) * p.inv_sqrt_k + kRmsEps;
+    barrier_lds();
+  }
+  if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
+}
+
+template <class TL, int EPI>
+hipError_t launch_x3(const GemmArgs& a, hipStream_t st) {
+  const int tiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
+  const dim3 block(TL::WN * TL::WM * TL::WK * 64);
+  if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true>), dim3(tiles), block, 0, st, a);
+  else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false>), dim3(tiles), block, 0, st, a);
+  return hipGetLastError();
+}
+
+template <class TL>
+hipError_t launch_x3_epi(const GemmArgs& a, int epi, hipStream_t st) {
+  if (!a.W3 || a.a_bf16 || a.c_bf16 || a.rpg || a.M <= 0 || a.N % TL::BNW || a.K % (32 * TL::WK) || a.lda % 4 ||
+      a.ldc % 4)
+    return hipErrorInvalidValue;
+  constexpr bool pairable = (TL::BNW / TL::WN / 32) % 2 == 0;   // g/u 32-row blocks in one wave tile
+  switch (epi) {
+    case EPI_STORE: return launch_x3<TL, EPI_STORE>(a, st);
+    case EPI_RESID: return launch_x3<TL, EPI_RESID>(a, st);
+    case EPI_SWIGLU: if constexpr (pairable) return launch_x3<TL, EPI_SWIGLU>(a, st); else return hipErrorInvalidValue;
+    case EPI_GLU: if constexpr (pairable) return launch_x3<TL, EPI_GLU>(a, st); else return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
 int num_cus_t() {
   static int n = 0;
   if (!n) {
@@ -705,6 +959,22 @@ hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     case 3: return launch_t_epi<TT<128, 128, 2, 4>>(a, epi, st);
     case 4: return launch_t2_epi<TT<256, 128, 2, 2>>(a, epi, st);   // 2 workgroups per CU
     case 5: return launch_t2_epi<TT<128, 128, 2, 2>>(a, epi, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// fp32-by-split variants (LDS per workgroup): 0 = 64x64, 8 waves (2n x 2m x 2k), 3 stages (120 KiB);
+// 1 = 128x64, 8 waves, 2 stages (128 KiB, paired epilogues); 2 = 64x128, 8 waves, 2 stages
+// (112 KiB); 3 = 128x128, 4 waves (no K split), 3 stages (120 KiB); 4 = 64x64, 4 waves, 3 stages
+// (60 KiB, 2 workgroups per CU); 5 = 128x64, 4 waves, 3 stages (96 KiB, paired epilogues)
+hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st) {
+  switch (variant) {
+    case 0: return launch_x3_epi<XT<64, 64, 2, 2, 2, 3>>(a, epi, st);
+    case 1: return launch_x3_epi<XT<128, 64, 2, 2, 2, 2>>(a, epi, st);
+    case 2: return launch_x3_epi<XT<64, 128, 2, 2, 2, 2>>(a, epi, st);
+    case 3: return launch_x3_epi<XT<128, 128, 2, 2, 1, 3>>(a, epi, st);
+    case 4: return launch_x3_epi<XT<64, 64, 2, 2, 1, 3>>(a, epi, st);
+    case 5: return launch_x3_epi<XT<128, 64, 2, 2, 1, 3>>(a, epi, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -38,6 +38,7 @@ struct GemmArgs {
   int order_n;        // bf16 LDS-DMA kernel: XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8) (large W)
   int nt_store;       // non-temporal epilogue stores
   int dbg;            // microbenchmark only: 1 = no epilogue, 4 = no K loop
+  const uint16_t* W3; // fp32 mode: W split into three bf16 planes [3][N][K] (gemm_x3), or nullptr
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -47,6 +48,8 @@ hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit
 hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
+// fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3
+hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 
 // a3 conv2 as an implicit GEMM over all streams: A rows gathered from the channels-last
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,
@@ -65,8 +68,9 @@ hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, h
 
 // a3 part 1: pre-norm RMSNorm(64) + sub1 state + Conv2d(1->32,k11x21) + BN + SiLU, written with the
 // carried sub2 rows as the channels-last conv2 input x2 [B][38][44][32]; next sub1/sub2 states.
-hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const float* scale1,
-                       const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st);
+// w1: fp32 [32][11][21] (fp32 mode); w1t: bf16 [11][32][32] kf-padded (bf16 mode)
+hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
+                       const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st);
 
 // In-place RMSNorm over rows of 384 (norm_out, out_norm); optional bf16 shadow of the result.
 hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, hipStream_t st);

@@ -82,6 +82,7 @@ struct tone_session {
   // weights
   float *basis_p, *fbank_p, *rope_cos, *rope_sin;
   float *pre_norm, *w1, *scale1, *shift1, *scale2, *shift2, *out_norm;
+  void* w1t = nullptr;   // bf16 mode: conv1 weights [kt 11][c 32][kf 32] (kf >= 21 zero)
   void* w2c;
   void* wsub_out;
   float *wred, *bred, *bred_pw;
@@ -323,7 +324,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   LAUNCH("mel_prep", launch_mel_prep(signal, sr, s->wave, B, st));
   LAUNCH("mel", mel_gemms(s->wave, s->basis_p, s->fbank_p, s->power, s->feats, B, st));
   if (s->debug_stop == 0) return TONE_OK;
-  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->scale1, s->shift1, s->x2, bf, B, st));
+  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B, st));
   LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * kT, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
@@ -476,6 +477,13 @@ int finalize_weights(tone_session* s) {
       sh[c] = (float)(((double)(*c1b)[c] - (double)(*bn1[2])[c]) * scale + (double)(*bn1[1])[c]);
     }
     CALL(upload(s, &s->w1, *c1w));
+    if (s->precision == TONE_PRECISION_BF16) {
+      std::vector<float> wt((size_t)kSub1Kt * kSub1C * 32, 0.f);
+      for (int c = 0; c < kSub1C; ++c)
+        for (int kt = 0; kt < kSub1Kt; ++kt)
+          for (int kf = 0; kf < kSub1Kf; ++kf) wt[((size_t)kt * kSub1C + c) * 32 + kf] = (*c1w)[((size_t)c * kSub1Kt + kt) * kSub1Kf + kf];
+      CALL(upload_w(s, &s->w1t, wt));
+    }
     CALL(upload(s, &s->scale1, sc));
     CALL(upload(s, &s->shift1, sh));
   }
