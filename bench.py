@@ -29,7 +29,10 @@ from tone_amd.shard import gather_logprobs  # noqa: E402
 from tone_amd.weights import synthetic_weights  # noqa: E402
 
 METRIC = "real-time-factor & streams/sec/node, 300 ms chunk, batch=1..4096"
-PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"fp32": 157.3, "fp32-mfma": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+# "fp32" runs its GEMMs as exact 3-way bf16 splits: 6 bf16 MFMA products per fp32 multiply-add, so the
+# matrix pipe's own ceiling for that arithmetic is the bf16 dense peak / 6
+SPLIT_PIPE_PEAK = 2500.0 / 6
 HBM_PEAK_GBS = 8000.0
 
 # GEMM families and their algorithmic FLOP per step (per stream-chunk, x batch), for the roofline
@@ -77,7 +80,7 @@ def algo_bytes(family: str, precision: str, batch: int) -> float:
     family's launches in one step (only the FFN up-projection is modelled)."""
     if family != "gemm_ffn_up":
         return 0.0
-    e = 4 if precision == "fp32" else 2
+    e = 2 if precision == "bf16" else 4
     d, ff = C.D_MODEL, C.D_FF
     per = [e * (batch * C.layer_frames(l) * d + 2 * ff * d + batch * C.layer_frames(l) * ff)
            for l in range(C.N_LAYERS) for _ in range(2)]
@@ -187,6 +190,11 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True)
                 "avg_us": round(f["avg_us"], 2), "flop_per_launch": int(f["flop_per_launch"]),
                 "step_tflops": round(C.FLOP_PER_CHUNK * B / (elapsed / args.steps) / 1e12, 2),
                 "families_us_per_step": {k: round(v["avg_us"] * v["launches_per_step"], 1) for k, v in fams.items()}}
+        if precision == "fp32":
+            roof["gemm_arith"] = ("fp32 as exact 3-way bf16 splits, 6 products per multiply-add on "
+                                  "v_mfma_f32_32x32x16_bf16 (fp32-accurate; tests/test_gpu_parity.py)")
+            roof["pipe_peak"] = round(SPLIT_PIPE_PEAK, 1)
+            roof["pipe_frac"] = round(achieved / SPLIT_PIPE_PEAK, 4)
     sess.close()
     del slabs, pcm
     torch.cuda.empty_cache()
@@ -199,7 +207,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="streams per GPU (BASELINE config 2: 256)")
-    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "bf16"], default="fp32")
     ap.add_argument("--chunks", type=int, default=10, help="distinct 300 ms chunks cycled per stream")
     ap.add_argument("--cpu-baseline-s", type=float, default=12.0, help="CPU oracle budget (0 = skip)")
     ap.add_argument("--cpu-baseline-batch", type=int, default=32)

@@ -40,8 +40,10 @@ extern "C" {
 
 /* precision of the dense contractions; everything else (norms, softmax, log-softmax, state
  * arithmetic) is fp32 in every mode, and the state is fp16 at the boundary. */
-#define TONE_PRECISION_FP32 0 /* fp32 MFMA (v_mfma_f32_32x32x2_f32), BASELINE config 2 */
-#define TONE_PRECISION_BF16 1 /* bf16 MFMA, fp32 accumulate, BASELINE config 3       */
+#define TONE_PRECISION_FP32 0      /* fp32 GEMMs as exact 3-way bf16 splits (6 products, fp32 accumulate) */
+                                   /* on v_mfma_f32_32x32x16_bf16: fp32-accurate, BASELINE config 2      */
+#define TONE_PRECISION_BF16 1      /* bf16 MFMA operands, fp32 accumulate, BASELINE config 3            */
+#define TONE_PRECISION_FP32_MFMA 2 /* fp32 GEMMs on the exact-fp32 MFMA (v_mfma_f32_32x32x2_f32)       */
 
 #define TONE_OK 0
 #define TONE_E_INVALID -1   /* bad argument (shape, null pointer, unknown name)       */

@@ -662,12 +662,20 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   const int wk = wid / (WN * WM), wr = wid % (WN * WM), wn = wr / WM, wm = wr % WM;
   const int lr = lane & 31, lh = lane >> 5;
   const int ntn = p.N / BNW;
-  int wgid = blockIdx.x;
-  {  // XCD-contiguous tile order (bijective for any grid size)
-    const int nwg = gridDim.x, xcd = wgid & 7, q = nwg >> 3, rr = nwg & 7;
-    wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (wgid >> 3);
+  int m0, n0;
+  if ((ntn & 7) == 0) {
+    // large W (FFN up: 7 MB of planes > one XCD's 4 MB L2): XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8)
+    // for every M-tile, so each W plane row is fetched into one L2 only and the X tile is reused
+    // by the XCD's N-tiles back to back
+    const int npx = ntn >> 3, li = blockIdx.x >> 3;
+    m0 = (li / npx) * BMX;
+    n0 = ((blockIdx.x & 7) * npx + li % npx) * BNW;
+  } else {  // XCD-contiguous tile order (bijective for any grid size): an XCD shares each X tile
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (blockIdx.x >> 3);
+    m0 = (wgid / ntn) * BMX;
+    n0 = (wgid % ntn) * BNW;
   }
-  const int m0 = (wgid / ntn) * BMX, n0 = (wgid % ntn) * BNW;
   const int nk = p.K / (32 * WK);
   const float* __restrict__ X = static_cast<const float*>(p.A);
   const uint16_t* __restrict__ W3 = p.W3;

@@ -89,6 +89,7 @@ struct tone_session {
   void* wred_pw;
   float *whead, *bhead;
   LayerW L[16];
+  std::map<const void*, const uint16_t*> w3;   // fp32 (split) mode: GEMM weight -> its bf16 planes
 
   // activations
   float *wave, *power, *feats, *rA, *rB, *qkv, *kvp, *g, *probs;
@@ -147,13 +148,38 @@ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
-// GEMM weight in the session's precision (fp32, or bf16 bits)
+float bf2f(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// GEMM weight in the session's precision (fp32, or bf16 bits).  fp32 (split) mode also uploads the
+// exact three-term bf16 split [3][N][K] (w = w0 + w1 + w2, each term the bf16 rounding of what the
+// previous ones leave) that gemm_x3 reads.
 int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
-  if (s->precision == TONE_PRECISION_FP32) {
+  if (s->precision != TONE_PRECISION_BF16) {
     float* p;
     int rc = upload(s, &p, v);
     *out = p;
-    return rc;
+    if (rc || s->precision != TONE_PRECISION_FP32) return rc;
+    const size_t n = v.size();
+    std::vector<uint16_t> pl(3 * n);
+    for (size_t i = 0; i < n; ++i) {
+      const uint16_t h = f2bf(v[i]);
+      const float r1 = v[i] - bf2f(h);
+      const uint16_t m = f2bf(r1);
+      pl[i] = h;
+      pl[n + i] = m;
+      pl[2 * n + i] = f2bf(r1 - bf2f(m));
+    }
+    uint16_t* d;
+    rc = dalloc(s, &d, pl.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(d, pl.data(), pl.size() * 2, hipMemcpyHostToDevice));
+    s->w3[p] = d;
+    return TONE_OK;
   }
   std::vector<uint16_t> hb(v.size());
   for (size_t i = 0; i < v.size(); ++i) hb[i] = f2bf(v[i]);
@@ -303,6 +329,10 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   a.a_bf16 = bf && a_bf16;
   a.c_bf16 = bf && c_bf16;
   a.C2 = bf ? c2 : nullptr;
+  if (s->precision == TONE_PRECISION_FP32) {
+    auto it = s->w3.find(W);
+    a.W3 = it == s->w3.end() ? nullptr : it->second;
+  }
   LAUNCH(fam, gemm(a, epi, s->precision == TONE_PRECISION_BF16, st));
   return TONE_OK;
 }
@@ -720,7 +750,7 @@ const char* tone_last_error(void) { return g_err.c_str(); }
 
 int tone_session_create(tone_session** out, int device, int precision, int max_batch) {
   if (!out) return fail(TONE_E_INVALID, "null out pointer");
-  if (precision != TONE_PRECISION_FP32 && precision != TONE_PRECISION_BF16)
+  if (precision != TONE_PRECISION_FP32 && precision != TONE_PRECISION_BF16 && precision != TONE_PRECISION_FP32_MFMA)
     return fail(TONE_E_INVALID, "unknown precision " + std::to_string(precision));
   if (max_batch <= 0) return fail(TONE_E_INVALID, "max_batch must be positive");
   int n = 0;

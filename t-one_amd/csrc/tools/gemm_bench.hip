@@ -1,7 +1,8 @@
 // Microbenchmark + self-check of the bf16 GEMM tile/stage variants at the encoder's shapes.
 //   gemm_bench M K N epi variants [nsplit] [iters]      (epi: 0 STORE 1 RESID 2 SWIGLU 3 GLU)
 // Prints one JSON line per variant: average launch time, TFLOP/s and max |err| against a naive
-// fp32-accumulate kernel on the same bf16 operands.
+// fp32-accumulate kernel on the same bf16 operands (FULLF32=1: full fp32 operands, fp64 reference;
+// meaningful for the fp32 variants -2/-3, 30-33 and the split variants 50-55).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -52,6 +53,35 @@ __global__ void ref_kernel(const uint16_t* A, const uint16_t* W, const float* bi
   out[(int64_t)m * nout + o] = v;
 }
 
+// fp64 reference on fp32 operands (FULLF32=1: operands are full-precision fp32, not bf16 values)
+__global__ void ref64_kernel(const float* A, const float* W, const float* bias, const float* R, float* out, int M,
+                             int N, int K, int epi, int rowscale) {
+  const int m = blockIdx.y, o = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nout = (epi >= 2) ? N / 2 : N;
+  if (o >= nout) return;
+  double den = 1.0;
+  if (rowscale) {
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) s += (double)A[(int64_t)m * K + k] * A[(int64_t)m * K + k];
+    den = sqrt(s) / sqrt((double)K) + 1e-8;
+  }
+  auto dot = [&](int n) {
+    double acc = 0.0;
+    for (int k = 0; k < K; ++k) acc += (double)A[(int64_t)m * K + k] * W[(int64_t)n * K + k];
+    return acc / den + bias[n];
+  };
+  double v;
+  if (epi <= 1) {
+    v = dot(o);
+    if (epi == 1) v = R[(int64_t)m * N + o] + v;
+  } else {
+    const int blk = o / 32, c = o % 32, n0 = blk * 64 + c;
+    const double g = dot(n0), u = dot(n0 + 32);
+    v = (epi == 2) ? g / (1.0 + exp(-g)) * u : g / (1.0 + exp(-u));
+  }
+  out[(int64_t)m * nout + o] = (float)v;
+}
+
 __global__ void err_kernel(const void* C, int cbf, const float* ref, int64_t n, float* err) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float e = 0.f;
@@ -89,21 +119,38 @@ int main(int argc, char** argv) {
   float* ws_ss;
   CK(hipMalloc(&ws_ss, (size_t)16 * M * 4));   // split-K row sums of squares (rowscale)
   // fp32 copies of the same (bf16-representable) operands for the fp32 path (variant -2)
+  // FULLF32=1: full-precision fp32 operands and an fp64 reference (fp32 / x3 variants only)
+  const int fullf32 = getenv("FULLF32") ? atoi(getenv("FULLF32")) : 0;
   float *Af, *Wf;
+  uint16_t* W3;   // the three bf16 planes of Wf (gemm_x3)
   {
     std::vector<float> fa(hA.size()), fw(hW.size());
     for (size_t i = 0; i < hA.size(); ++i) { uint32_t u = (uint32_t)hA[i] << 16; memcpy(&fa[i], &u, 4); }
     for (size_t i = 0; i < hW.size(); ++i) { uint32_t u = (uint32_t)hW[i] << 16; memcpy(&fw[i], &u, 4); }
-    CK(hipMalloc(&Af, fa.size() * 4)); CK(hipMalloc(&Wf, fw.size() * 4));
+    if (fullf32) {
+      for (auto& v : fa) v = rnd();
+      for (auto& v : fw) v = rnd() * 0.05f;
+    }
+    std::vector<uint16_t> w3(3 * fw.size());
+    auto bf2f = [](uint16_t h) { uint32_t u = (uint32_t)h << 16; float f; memcpy(&f, &u, 4); return f; };
+    for (size_t i = 0; i < fw.size(); ++i) {
+      const uint16_t h = to_bf16(fw[i]);
+      const float r1 = fw[i] - bf2f(h);
+      const uint16_t m = to_bf16(r1);
+      w3[i] = h; w3[fw.size() + i] = m; w3[2 * fw.size() + i] = to_bf16(r1 - bf2f(m));
+    }
+    CK(hipMalloc(&Af, fa.size() * 4)); CK(hipMalloc(&Wf, fw.size() * 4)); CK(hipMalloc(&W3, w3.size() * 2));
     CK(hipMemcpy(Af, fa.data(), fa.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(Wf, fw.data(), fw.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(W3, w3.data(), w3.size() * 2, hipMemcpyHostToDevice));
   }
   CK(hipMemcpy(A, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(W, hW.data(), hW.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(bias, hb.data(), N * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(R, hR.data(), hR.size() * 4, hipMemcpyHostToDevice));
   const int rowscale = getenv("ROWSCALE") ? atoi(getenv("ROWSCALE")) : 0;
-  hipLaunchKernelGGL(ref_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, A, W, bias, R, ref, M, N, K, epi, rowscale);
+  if (fullf32) hipLaunchKernelGGL(ref64_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, Af, Wf, bias, R, ref, M, N, K, epi, rowscale);
+  else hipLaunchKernelGGL(ref_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, A, W, bias, R, ref, M, N, K, epi, rowscale);
   CK(hipDeviceSynchronize());
 
   GemmArgs a{};
@@ -120,20 +167,22 @@ int main(int argc, char** argv) {
     const int vv = atoi(tok);
     // v % 100 = variant (20..23: gemm_t tiles); (v / 100) bits: 1 N-partitioned XCD order,
     // 2 non-temporal stores, 4.. debug (no epilogue / no K loop)
-    const int v = vv < 0 ? vv : (vv % 100);
+    const int v = vv < 0 ? vv : (vv % 100);   // -1 gemm() bf16, -2 gemm() fp32 (+W3), -3 gemm() fp32 (no W3)
     const int fl = vv < 0 ? 0 : vv / 100;
     a.order_n = fl & 1;
     a.nt_store = (fl >> 1) & 1;
     a.dbg = (fl >> 2) & 7;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
-    const bool f32 = (vv == -2) || (v >= 30 && v < 40);
+    const bool f32 = (vv == -2) || (vv == -3) || (v >= 30 && v < 40) || (v >= 50 && v < 60);
+    a.W3 = (vv == -2 || (v >= 50 && v < 60)) ? W3 : nullptr;   // -2: gemm() fp32 routing with planes, -3: without
     a.A = f32 ? (const void*)Af : (const void*)A;
     a.W = f32 ? (const void*)Wf : (const void*)W;
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
       return v < 0 ? gemm(a, epi, !f32, 0)
+             : v >= 50 ? gemm_x3(a, epi, v - 50, 0)
              : v >= 40 ? gemm_f32t(a, epi, v - 40, 0)
              : v >= 30 ? gemm_f32t(a, epi, v - 30, 0)
              : v >= 20 ? gemm_t(a, epi, v - 20, 0)

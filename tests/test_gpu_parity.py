@@ -222,6 +222,32 @@ def test_numpy_dropin_matches_session(weights):
     model.session.close()
 
 
+def test_fp32_split_vs_fp32_mfma(weights, oracle):
+    """The default fp32 path computes its GEMMs as exact 3-way bf16 splits on the bf16 MFMA
+    (gemm_t.hip gemm_x3); "fp32-mfma" uses v_mfma_f32_32x32x2_f32.  Both must meet the fp32 bar
+    against the oracle, and the split path must be no less accurate than the exact-fp32 MFMA one."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    rng = np.random.default_rng(21)
+    b = 32
+    pcm = [synthetic_pcm(rng, b) for _ in range(3)]
+    errs = {}
+    for prec in ("fp32", "fp32-mfma"):
+        s = ToneSession(weights, precision=prec, max_batch=b)
+        st = np.zeros((b, C.STATE_SIZE), np.float16)
+        worst = 0.0
+        for c in range(3):
+            lp_g, st_g = gpu_step(s, pcm[c], st)
+            lp_o, st_o = oracle.step(pcm[c], st)
+            assert_logp_close(lp_g, lp_o, what=f"{prec} chunk {c}")
+            assert_state_close(st_g, st_o, what=f"{prec} chunk {c}")
+            worst = max(worst, float(np.abs(lp_g - lp_o).max()))
+            st = st_g
+        s.close()
+        errs[prec] = worst
+    assert errs["fp32"] <= 2 * errs["fp32-mfma"] + 1e-5, errs
+
+
 def test_bf16_mode_close_to_oracle(weights, oracle):
     """BASELINE config 3 arithmetic: bf16 MFMA operands, fp32 accumulate/norms/softmax."""
     _gpu()
