@@ -88,5 +88,26 @@ __device__ __forceinline__ void store_bf16(uint16_t* base, int64_t i, float v) {
   __bf16 h = (__bf16)v;
   base[i] = __builtin_bit_cast(uint16_t, h);
 }
+// Exact three-term bf16 split of an fp32 value: v = t0 + t1 + t2, t0 = bf16(v), t1 = bf16(v - t0),
+// t2 = bf16(v - t0 - t1) (both residuals exact in fp32; |v - t0 - t1 - t2| <= 2^-27 |v|).
+__device__ __forceinline__ void split3_f(float v, float& t0, float& t1, float& t2) {
+  t0 = (float)(__bf16)v;
+  const float r = v - t0;
+  t1 = (float)(__bf16)r;
+  t2 = (float)(__bf16)(r - t1);
+}
+// bf16 shadow of an fp32 activation for the next GEMM's A operand: one plane (bf16 mode), or with
+// plane > 0 the exact split into planes s, s + plane, s + 2 plane (fp32 split mode, gemm_x3).
+__device__ __forceinline__ void store_shadow(uint16_t* s, int64_t plane, int64_t i, float v) {
+  if (!plane) {
+    store_bf16(s, i, v);
+    return;
+  }
+  float t0, t1, t2;
+  split3_f(v, t0, t1, t2);
+  store_bf16(s, i, t0);
+  store_bf16(s, i + plane, t1);
+  store_bf16(s, i + 2 * plane, t2);
+}
 
 }  // namespace tone

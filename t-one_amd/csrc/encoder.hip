@@ -10,7 +10,7 @@ constexpr float kInvSqrtD = 0.05103103630798288f;   // 384^-0.5 (submodules.py:5
 // ---------------------------------------------------------------------------------------------
 // RMSNorm (submodules.py:34-54) in place over rows of 384: one wave per row, 6 elements per lane.
 __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, const float* __restrict__ w, int rows,
-                                                      uint16_t* __restrict__ shadow) {
+                                                      uint16_t* __restrict__ shadow, int64_t plane) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -28,12 +28,12 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, con
   for (int i = 0; i < 6; ++i) {
     const float y = w[lane + 64 * i] * (v[i] / den);
     xr[lane + 64 * i] = y;
-    if (shadow) store_bf16(shadow, (int64_t)row * kD + lane + 64 * i, y);
+    if (shadow) store_shadow(shadow, plane, (int64_t)row * kD + lane + 64 * i, y);
   }
 }
 
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, hipStream_t st) {
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow);
+hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st) {
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane);
   return hipGetLastError();
 }
 
@@ -370,7 +370,7 @@ hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const 
 // ---------------------------------------------------------------------------------------------
 // TemporalUpsampling (conformer_blocks.py:955-988): repeat_interleave x2, trim to 10, + residual.
 __global__ void __launch_bounds__(256) upsample_add_kernel(float* __restrict__ x10, const float* __restrict__ x5, int B,
-                                                           uint16_t* __restrict__ shadow) {
+                                                           uint16_t* __restrict__ shadow, int64_t plane) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)B * kT * kD) return;
   const int64_t row = idx / kD;
@@ -378,12 +378,13 @@ __global__ void __launch_bounds__(256) upsample_add_kernel(float* __restrict__ x
   const int64_t b = row / kT, t = row % kT;
   const float v = x5[(b * (kT / 2) + t / 2) * kD + c] + x10[idx];
   x10[idx] = v;
-  if (shadow) store_bf16(shadow, idx, v);
+  if (shadow) store_shadow(shadow, plane, idx, v);
 }
 
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, hipStream_t st) {
+hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, int64_t plane, hipStream_t st) {
   const int64_t n = (int64_t)B * kT * kD;
-  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, shadow);
+  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, shadow,
+                     plane);
   return hipGetLastError();
 }
 

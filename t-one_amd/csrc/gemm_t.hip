@@ -87,6 +87,16 @@ __device__ __forceinline__ void store_tile_bf16(uint16_t* rowp, const float (&v)
   }
 }
 
+// The same 16 values stored as their exact 3-term bf16 split into three planes `plane` apart.
+__device__ __forceinline__ void store_tile_split(uint16_t* rowp, int64_t plane, const float (&v)[16], int lh, bool ok) {
+  float t0[16], t1[16], t2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) split3_f(v[r], t0[r], t1[r], t2[r]);
+  store_tile_bf16(rowp, t0, lh, ok);
+  store_tile_bf16(rowp + plane, t1, lh, ok);
+  store_tile_bf16(rowp + 2 * plane, t2, lh, ok);
+}
+
 // Per-tile epilogue shared by both kernels.  acc[i][j] is the wave's 32x32 D tile (n-tile i,
 // m-tile j); rd[m - m0] the row-scale denominators, sb[n - n0] the bias (both LDS).
 template <int EPI, bool RS, int TI, int TJ, int WTN, int WTM>
@@ -114,6 +124,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[T
         }
         if (p.c_bf16) {
           store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, o, lh, ok);
+        } else if (p.c_plane) {   // fp32 split mode: the next GEMM's A as 3 bf16 planes
+          store_tile_split(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, p.c_plane, o, lh, ok);
         } else {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
@@ -143,7 +155,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[T
             v[4 * g] = o.x; v[4 * g + 1] = o.y; v[4 * g + 2] = o.z; v[4 * g + 3] = o.w;
             if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
           }
-          if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);
+          if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
+          else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);
         } else if (p.c_bf16) {
           store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + nb, v, lh, ok);
         } else {
@@ -152,7 +165,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[T
             const f32x4 o = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
             if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
           }
-          if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);   // bf16 shadow (fp32 C)
+          if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
+          else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);   // bf16 shadow (fp32 C)
         }
       }
     }
@@ -637,15 +651,18 @@ __device__ __forceinline__ void split3(const f32x4 a, const f32x4 b, bf16x8& h, 
   }
 }
 
-template <class TL, int EPI, bool RS>
+// XS: X arrives pre-split (3 bf16 planes written by its producer, GemmArgs::a_plane) and is staged
+// like W -- no split VALU in the loop; otherwise X is fp32 and split from its LDS fragment.
+template <class TL, int EPI, bool RS, bool XS>
 __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(GemmArgs p) {
   constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, WK = TL::WK, S = TL::S;
   constexpr int NW = WN * WM * WK, NT = NW * 64;
   constexpr int WTN = BNW / WN, WTM = BMX / WM, TI = WTN / 32, TJ = WTM / 32;
   constexpr int WPL = BNW * 16;                                 // floats of one W plane slice (64-B rows)
-  constexpr int GROUP = 3 * WPL + BMX * 32;                     // floats of one wave group's slice
+  constexpr int XPL = BMX * 16;                                 // floats of one X plane slice (XS)
+  constexpr int GROUP = 3 * WPL + (XS ? 3 * XPL : BMX * 32);    // floats of one wave group's slice
   constexpr int STAGE = WK * GROUP;
-  constexpr int WPC = 3 * BNW / 16, XPC = BMX / 8;              // 1 KiB DMA pieces per group
+  constexpr int WPC = 3 * BNW / 16, XPC = XS ? 3 * BMX / 16 : BMX / 8;   // 1 KiB DMA pieces per group
   constexpr int PIECES = WK * (WPC + XPC), IPW = PIECES / NW;
   static_assert(PIECES % NW == 0 && IPW >= 1, "DMA pieces per wave");
   static_assert(TI >= 1 && TJ >= 1 && WN >= TJ, "wave tile / row-scale ownership");
@@ -678,6 +695,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   }
   const int nk = p.K / (32 * WK);
   const float* __restrict__ X = static_cast<const float*>(p.A);
+  const uint16_t* __restrict__ X3 = static_cast<const uint16_t*>(p.A);
   const uint16_t* __restrict__ W3 = p.W3;
   const int64_t plane = (int64_t)p.N * p.K;
 
@@ -699,6 +717,11 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
         const int slot = (lane & 3) ^ ((row >> 2) & 3);
         src = W3 + pl * plane + (int64_t)(n0 + row) * p.K + kb + slot * 8;
         dst = base + g * GROUP + pl * WPL + rb * 16;
+      } else if constexpr (XS) {                                // 16 X rows x 64 B of plane pl
+        const int xp = pr - WPC, pl = xp / (BMX / 16), rb = (xp % (BMX / 16)) * 16, row = rb + (lane >> 2);
+        const int slot = (lane & 3) ^ ((row >> 2) & 3);
+        src = X3 + pl * p.a_plane + (int64_t)min(m0 + row, p.M - 1) * p.lda + kb + slot * 8;
+        dst = base + g * GROUP + 3 * WPL + pl * XPL + rb * 16;
       } else {                                                  // 8 X rows x 128 B
         const int rb = (pr - WPC) * 8, row = rb + (lane >> 3);
         const int slot = (lane & 7) ^ ((row >> 1) & 7);
@@ -738,16 +761,39 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
         for (int pl = 0; pl < 3; ++pl)
           w[pl][i] = *reinterpret_cast<const bf16x8*>(base + pl * WPL + row * 16 + ((j8 ^ ((row >> 2) & 3)) << 2));
       }
+      if constexpr (XS) {
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
+        for (int j = 0; j < TJ; ++j) {
+          const int row = wm * WTM + 32 * j + lr;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            xs[pl][j] = *reinterpret_cast<const bf16x8*>(base + 3 * WPL + pl * XPL + row * 16 + ((j8 ^ ((row >> 2) & 3)) << 2));
+        }
+        if constexpr (RS) {   // ||x||^2 in fp32 from the reassembled values (x0 + x1 + x2 == x exactly)
+          bf16x8 a0 = xs[0][0], a1 = xs[1][0], a2 = xs[2][0];
+#pragma unroll
+          for (int j = 1; j < TJ; ++j) {
+            a0 = (jss == j) ? xs[0][j] : a0;
+            a1 = (jss == j) ? xs[1][j] : a1;
+            a2 = (jss == j) ? xs[2][j] : a2;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = ((float)a0[e] + (float)a1[e]) + (float)a2[e];
+            ss = fmaf(v, v, ss);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < (XS ? 0 : TJ); ++j) {
         const int row = wm * WTM + 32 * j + lr, cs = (row >> 1) & 7;
         const float* xr = base + 3 * WPL + row * 32;
         xv[j][0] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8) ^ cs) << 2));
         xv[j][1] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8 + 1) ^ cs) << 2));
       }
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) split3(xv[j][0], xv[j][1], xs[0][j], xs[1][j], xs[2][j]);
-      if constexpr (RS) {
+      for (int j = 0; j < (XS ? 0 : TJ); ++j) split3(xv[j][0], xv[j][1], xs[0][j], xs[1][j], xs[2][j]);
+      if constexpr (RS && !XS) {
         f32x4 a = xv[0][0], b = xv[0][1];
 #pragma unroll
         for (int j = 1; j < TJ; ++j) {
@@ -834,15 +880,21 @@ template <class TL, int EPI>
 hipError_t launch_x3(const GemmArgs& a, hipStream_t st) {
   const int tiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
-  if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true>), dim3(tiles), block, 0, st, a);
-  else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false>), dim3(tiles), block, 0, st, a);
+  if (a.a_plane) {
+    if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, true>), dim3(tiles), block, 0, st, a);
+    else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, true>), dim3(tiles), block, 0, st, a);
+  } else {
+    if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, false>), dim3(tiles), block, 0, st, a);
+    else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, false>), dim3(tiles), block, 0, st, a);
+  }
   return hipGetLastError();
 }
 
 template <class TL>
 hipError_t launch_x3_epi(const GemmArgs& a, int epi, hipStream_t st) {
-  if (!a.W3 || a.a_bf16 || a.c_bf16 || a.rpg || a.M <= 0 || a.N % TL::BNW || a.K % (32 * TL::WK) || a.lda % 4 ||
-      a.ldc % 4)
+  if (!a.W3 || a.a_bf16 || a.c_bf16 || a.rpg || a.M <= 0 || a.N % TL::BNW || a.K % (32 * TL::WK) || a.lda % 8 ||
+      a.ldc % 8 || (a.c_plane && (a.c_plane % 8 || (epi != EPI_SWIGLU && epi != EPI_GLU))) || a.c2_plane % 8 ||
+      a.a_plane % 8)
     return hipErrorInvalidValue;
   constexpr bool pairable = (TL::BNW / TL::WN / 32) % 2 == 0;   // g/u 32-row blocks in one wave tile
   switch (epi) {

@@ -39,6 +39,11 @@ struct GemmArgs {
   int nt_store;       // non-temporal epilogue stores
   int dbg;            // microbenchmark only: 1 = no epilogue, 4 = no K loop
   const uint16_t* W3; // fp32 mode: W split into three bf16 planes [3][N][K] (gemm_x3), or nullptr
+  // fp32 split mode (gemm_x3): an operand held as its exact 3-term bf16 split, planes `*_plane`
+  // elements apart (0 = not split)
+  int64_t a_plane;    // A given as 3 bf16 planes (lda in elements) instead of fp32
+  int64_t c_plane;    // STORE / SWIGLU / GLU: C written as 3 bf16 planes instead of fp32
+  int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -72,8 +77,9 @@ hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, h
 hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
                        const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st);
 
-// In-place RMSNorm over rows of 384 (norm_out, out_norm); optional bf16 shadow of the result.
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, hipStream_t st);
+// In-place RMSNorm over rows of 384 (norm_out, out_norm); optional bf16 shadow of the result
+// (3 split planes `plane` elements apart when plane > 0).
+hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st);
 
 // Layers 14/15: xn = RMSNorm(r); kv = [cache(S rows) ; xn]; next cache (left-padded to 30) -> state.
 hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S,
@@ -106,7 +112,7 @@ hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const 
                               hipStream_t st);
 
 // a12: x10[b*10+t] += x5[b*5+t/2]
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, hipStream_t st);
+hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, int64_t plane, hipStream_t st);
 
 // a14: logits = x . Wd^T + bd, log_softmax over 35 classes -> logprobs [B*10][35]
 // a14 + decode flags: logprobs [rows][35]; optional frame_info[row] = greedy token | speech flag << 8

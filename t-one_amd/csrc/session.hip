@@ -358,7 +358,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * kT, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
-  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, shA, st));
+  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, shA, 0, st));
   if (s->debug_stop == 1) return TONE_OK;
   float* x = s->rA;
   uint16_t* xs = shA;           // bf16 shadow of x (bf16 mode)
@@ -425,7 +425,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
                    1.0f, true, true));
     CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[1], x, D, w.b2[1], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
                    false, xs));
-    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, st));
+    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
       LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, st));
       CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * (kT / 2), D, 4 * D,
@@ -435,7 +435,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       T = kT / 2;
     }
     if (l == 14) {  // TemporalUpsampling (conformer.py:224-225)
-      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, shA, st));
+      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, shA, 0, st));
       x = s->rA;
       xs = shA;
       T = kT;

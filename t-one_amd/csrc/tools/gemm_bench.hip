@@ -123,6 +123,7 @@ int main(int argc, char** argv) {
   const int fullf32 = getenv("FULLF32") ? atoi(getenv("FULLF32")) : 0;
   float *Af, *Wf;
   uint16_t* W3;   // the three bf16 planes of Wf (gemm_x3)
+  uint16_t* A3;   // the three bf16 planes of Af (gemm_x3 with a pre-split A, variants 60-65)
   {
     std::vector<float> fa(hA.size()), fw(hW.size());
     for (size_t i = 0; i < hA.size(); ++i) { uint32_t u = (uint32_t)hA[i] << 16; memcpy(&fa[i], &u, 4); }
@@ -143,6 +144,15 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(Af, fa.data(), fa.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(Wf, fw.data(), fw.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(W3, w3.data(), w3.size() * 2, hipMemcpyHostToDevice));
+    std::vector<uint16_t> a3(3 * fa.size());
+    for (size_t i = 0; i < fa.size(); ++i) {
+      const uint16_t h = to_bf16(fa[i]);
+      const float r1 = fa[i] - bf2f(h);
+      const uint16_t m = to_bf16(r1);
+      a3[i] = h; a3[fa.size() + i] = m; a3[2 * fa.size() + i] = to_bf16(r1 - bf2f(m));
+    }
+    CK(hipMalloc(&A3, a3.size() * 2));
+    CK(hipMemcpy(A3, a3.data(), a3.size() * 2, hipMemcpyHostToDevice));
   }
   CK(hipMemcpy(A, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(W, hW.data(), hW.size() * 2, hipMemcpyHostToDevice));
@@ -174,14 +184,17 @@ int main(int argc, char** argv) {
     a.dbg = (fl >> 2) & 7;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
-    const bool f32 = (vv == -2) || (vv == -3) || (v >= 30 && v < 40) || (v >= 50 && v < 60);
-    a.W3 = (vv == -2 || (v >= 50 && v < 60)) ? W3 : nullptr;   // -2: gemm() fp32 routing with planes, -3: without
-    a.A = f32 ? (const void*)Af : (const void*)A;
+    const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 40) || (v >= 50 && v < 70);
+    // -2: gemm() fp32 routing with W planes, -3: without, -4: with W and A planes
+    a.W3 = (vv == -2 || vv == -4 || (v >= 50 && v < 70)) ? W3 : nullptr;
+    a.a_plane = (vv == -4 || (v >= 60 && v < 70)) ? (int64_t)M * K : 0;
+    a.A = a.a_plane ? (const void*)A3 : f32 ? (const void*)Af : (const void*)A;
     a.W = f32 ? (const void*)Wf : (const void*)W;
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
       return v < 0 ? gemm(a, epi, !f32, 0)
+             : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
              : v >= 50 ? gemm_x3(a, epi, v - 50, 0)
              : v >= 40 ? gemm_f32t(a, epi, v - 40, 0)
              : v >= 30 ? gemm_f32t(a, epi, v - 30, 0)
