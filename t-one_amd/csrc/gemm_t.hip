@@ -747,35 +747,49 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   float ss = 0.f;
   const int jss = wn % TJ;                                      // m-tile whose sum of squares this wave keeps
 
+  // One K-step: every fragment of both 16-deep halves is read first (one LDS wait), then per half
+  // the X split (VALU) and the 6 x TI x TJ MFMAs, so the split of one half can issue under the
+  // MFMAs of the other.
   auto compute = [&](int buf) {
     const float* base = lds + buf * STAGE + wk * GROUP;
+    bf16x8 w[2][3][TI], xs[2][3][TJ];
+    f32x4 xv[2][TJ][2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int j8 = 2 * q + lh;                                // 8-value block of the 32-k slice
-      bf16x8 w[3][TI], xs[3][TJ];
-      f32x4 xv[TJ][2];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int row = wn * WTN + 32 * i + lr;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-          w[pl][i] = *reinterpret_cast<const bf16x8*>(base + pl * WPL + row * 16 + ((j8 ^ ((row >> 2) & 3)) << 2));
+          w[q][pl][i] = *reinterpret_cast<const bf16x8*>(base + pl * WPL + row * 16 + ((j8 ^ ((row >> 2) & 3)) << 2));
       }
-      if constexpr (XS) {
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) {
+      for (int j = 0; j < TJ; ++j) {
+        if constexpr (XS) {
           const int row = wm * WTM + 32 * j + lr;
 #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
-            xs[pl][j] = *reinterpret_cast<const bf16x8*>(base + 3 * WPL + pl * XPL + row * 16 + ((j8 ^ ((row >> 2) & 3)) << 2));
+            xs[q][pl][j] = *reinterpret_cast<const bf16x8*>(base + 3 * WPL + pl * XPL + row * 16 + ((j8 ^ ((row >> 2) & 3)) << 2));
+        } else {
+          const int row = wm * WTM + 32 * j + lr, cs = (row >> 1) & 7;
+          const float* xr = base + 3 * WPL + row * 32;
+          xv[q][j][0] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8) ^ cs) << 2));
+          xv[q][j][1] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8 + 1) ^ cs) << 2));
         }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead (hipcc sinks them to their uses)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if constexpr (XS) {
         if constexpr (RS) {   // ||x||^2 in fp32 from the reassembled values (x0 + x1 + x2 == x exactly)
-          bf16x8 a0 = xs[0][0], a1 = xs[1][0], a2 = xs[2][0];
+          bf16x8 a0 = xs[q][0][0], a1 = xs[q][1][0], a2 = xs[q][2][0];
 #pragma unroll
           for (int j = 1; j < TJ; ++j) {
-            a0 = (jss == j) ? xs[0][j] : a0;
-            a1 = (jss == j) ? xs[1][j] : a1;
-            a2 = (jss == j) ? xs[2][j] : a2;
+            a0 = (jss == j) ? xs[q][0][j] : a0;
+            a1 = (jss == j) ? xs[q][1][j] : a1;
+            a2 = (jss == j) ? xs[q][2][j] : a2;
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -783,36 +797,30 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
             ss = fmaf(v, v, ss);
           }
         }
-      }
+      } else {
 #pragma unroll
-      for (int j = 0; j < (XS ? 0 : TJ); ++j) {
-        const int row = wm * WTM + 32 * j + lr, cs = (row >> 1) & 7;
-        const float* xr = base + 3 * WPL + row * 32;
-        xv[j][0] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8) ^ cs) << 2));
-        xv[j][1] = *reinterpret_cast<const f32x4*>(xr + (((2 * j8 + 1) ^ cs) << 2));
-      }
+        for (int j = 0; j < TJ; ++j) split3(xv[q][j][0], xv[q][j][1], xs[q][0][j], xs[q][1][j], xs[q][2][j]);
+        if constexpr (RS) {
+          f32x4 a = xv[q][0][0], b = xv[q][0][1];
 #pragma unroll
-      for (int j = 0; j < (XS ? 0 : TJ); ++j) split3(xv[j][0], xv[j][1], xs[0][j], xs[1][j], xs[2][j]);
-      if constexpr (RS && !XS) {
-        f32x4 a = xv[0][0], b = xv[0][1];
-#pragma unroll
-        for (int j = 1; j < TJ; ++j) {
-          a = (jss == j) ? xv[j][0] : a;
-          b = (jss == j) ? xv[j][1] : b;
+          for (int j = 1; j < TJ; ++j) {
+            a = (jss == j) ? xv[q][j][0] : a;
+            b = (jss == j) ? xv[q][j][1] : b;
+          }
+          ss = fmaf(a.x, a.x, ss); ss = fmaf(a.y, a.y, ss); ss = fmaf(a.z, a.z, ss); ss = fmaf(a.w, a.w, ss);
+          ss = fmaf(b.x, b.x, ss); ss = fmaf(b.y, b.y, ss); ss = fmaf(b.z, b.z, ss); ss = fmaf(b.w, b.w, ss);
         }
-        ss = fmaf(a.x, a.x, ss); ss = fmaf(a.y, a.y, ss); ss = fmaf(a.z, a.z, ss); ss = fmaf(a.w, a.w, ss);
-        ss = fmaf(b.x, b.x, ss); ss = fmaf(b.y, b.y, ss); ss = fmaf(b.z, b.z, ss); ss = fmaf(b.w, b.w, ss);
       }
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {   // small terms first
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2][i], xs[0][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1][i], xs[1][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0][i], xs[2][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1][i], xs[0][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0][i], xs[1][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0][i], xs[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[q][2][i], xs[q][0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[q][1][i], xs[q][1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[q][0][i], xs[q][2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[q][1][i], xs[q][0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[q][0][i], xs[q][1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[q][0][i], xs[q][0][j], acc[i][j], 0, 0, 0);
         }
     }
   };
