@@ -6,6 +6,7 @@ Drop-in for ``tone.onnx_wrapper.StreamingCTCModel`` (the acoustic model slot of
 """
 
 from . import config  # noqa: F401
+from .state import flat_to_triton, triton_to_flat  # noqa: F401  (Triton cache_last_* interop)
 
 __version__ = "0.1.0"
 
