@@ -173,14 +173,25 @@ def test_slot_pipeline_matches_sequential_streams(session):
         session.set_frame_info(None)
 
 
-@pytest.mark.gpu
-def test_forward_offline_matches_oracle_decode(session):
-    """Offline decoding of one utterance: phrases from device frame info == the oracle's splitter +
-    greedy decoder run on the device logprobs of the same steps."""
-    import torch
+def _example_audio():
+    return np.load(Path(__file__).parent / "golden" / "audio_short_pcm.npy").astype(np.int32)
+
+
+def _noise_audio():
     rng = np.random.default_rng(3)
     audio = np.clip(rng.normal(0, 2500, 8000 * 4), -32768, 32767).astype(np.int32)
     audio[8000:16000] = 0
+    return audio
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("make_audio", [_noise_audio, _example_audio], ids=["noise", "example_audio"])
+def test_forward_offline_matches_oracle_decode(session, make_audio):
+    """Offline decoding of one utterance (synthetic, and the reference's example audio_short.flac):
+    phrases from device frame info == the oracle's splitter + greedy decoder run on the device
+    logprobs of the same steps."""
+    import torch
+    audio = make_audio()
     pipe = P.StreamingGreedyPipeline(session, n_slots=2)
     got = pipe.forward_offline(audio)
     # replay: same chunks through session.step, oracle decode on the logprobs

@@ -122,6 +122,24 @@ def test_golden_stream_parity(sess, oracle):
         st_gpu = st_g
 
 
+def test_example_audio_parity(sess, oracle):
+    """The reference's example utterance (tests/golden/audio_short_pcm.npy: the MD5-pinned decode of
+    tone/demo/audio_examples/audio_short.flac) fed as the pipeline feeds it -- 300 ms of padding on
+    both sides, whole 2400-sample chunks (tone/pipeline.py:178-200) -- beside its polarity-inverted
+    copy; every chunk's logprobs vs the oracle stepped from the same state, <= 1e-3."""
+    pcm = np.load(GOLDEN / "audio_short_pcm.npy").astype(np.int32)
+    a = np.pad(pcm, (C.AUDIO_CHUNK_SAMPLES, C.AUDIO_CHUNK_SAMPLES))
+    a = np.pad(a, (0, -len(a) % C.AUDIO_CHUNK_SAMPLES)).reshape(-1, C.AUDIO_CHUNK_SAMPLES)
+    chunks = np.stack([a, np.clip(-a, -32768, 32767)], 1)
+    st = np.zeros((2, C.STATE_SIZE), np.float16)
+    for c in range(len(chunks)):
+        lp_g, st_g = gpu_step(sess, chunks[c], st)
+        lp_o, st_o = oracle.step(chunks[c], st)
+        assert_logp_close(lp_g, lp_o, what=f"example audio chunk {c}")
+        assert_state_close(st_g, st_o, what=f"example audio chunk {c}")
+        st = st_g
+
+
 def test_b256_parity(sess, oracle):
     """BASELINE config 2: batch 256, fp32, logprobs vs the CPU oracle <= 1e-3 over 3 chunks."""
     rng = np.random.default_rng(11)
