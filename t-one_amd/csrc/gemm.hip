@@ -1021,9 +1021,13 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   if (!bf16 && a.W3 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
     // fp32 by exact bf16 splitting (gemm_t.hip gemm_x3); tile per shape from tools/gemm_bench
     // (scripts/x3_sweep.sh, profiles/r01_x3_sweep_b256.jsonl)
-    if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 3, st);
+    // (scripts/x3_sweep.sh, scripts/x3w_sweep.sh; profiles/r01_x3_*.jsonl)
+    if (epi == EPI_SWIGLU && a.N % 256 == 0)
+      return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200 ? 7 : 6, st);
+    if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
     if (epi == EPI_GLU && a.N % 128 == 0) return gemm_x3(a, epi, 1, st);
-    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_x3(a, epi, a.N >= 1024 ? 4 : 0, st);
+    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N >= 1024 && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
+    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_x3(a, epi, 0, st);
   }
   if (!bf16 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
     // exact-fp32 projections other than the FFN up-projection: in-workgroup K split (gemm_t.hip)

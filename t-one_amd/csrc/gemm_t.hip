@@ -1043,6 +1043,10 @@ hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     case 3: return launch_x3_epi<XT<128, 128, 2, 2, 1, 3>>(a, epi, st);
     case 4: return launch_x3_epi<XT<64, 64, 2, 2, 1, 3>>(a, epi, st);
     case 5: return launch_x3_epi<XT<128, 64, 2, 2, 1, 3>>(a, epi, st);
+    // two waves per SIMD (one wave issues its LDS-DMA pieces while the other runs MFMAs)
+    case 6: return launch_x3_epi<XT<128, 128, 2, 4, 1, 3>>(a, epi, st);   // 8 waves, 120 KiB
+    case 7: return launch_x3_epi<XT<256, 128, 4, 2, 1, 2>>(a, epi, st);   // 8 waves, 128 KiB
+    case 8: return launch_x3_epi<XT<128, 256, 2, 4, 1, 2>>(a, epi, st);   // 8 waves, 112 KiB
     default: return hipErrorInvalidValue;
   }
 }
