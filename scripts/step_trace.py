@@ -1,12 +1,12 @@
 """Per-dispatch durations of the last full step in a rocprofv3 kernel trace (grouped by kernel)."""
-import collections, csv, sys
+import collections, csv, re, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 seq = [(r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000) for r in rows]
 idx = [i for i, (n, _) in enumerate(seq) if "mel_prep" in n]
 st, en = idx[-2], idx[-1]
 agg = collections.defaultdict(lambda: [0, 0.0])
 for n, d in seq[st:en]:
-    k = n.split("(")[0][:90]
+    k = re.sub(r"\([^()]*\)$", "", n).replace("(anonymous namespace)::", "")[:110]
     agg[k][0] += 1
     agg[k][1] += d
 tot = sum(v[1] for v in agg.values())
