@@ -1012,6 +1012,32 @@ hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit
   }
 }
 
+// Split fp32 (gemm_x3) with the K range split over nsplit workgroups: raw partials into a.ws, then
+// the fixed-order combine + epilogue (bias, residual, alpha) -- for the small-M, large-K projections
+// (FFN down at B = 256: 60 tiles of 128 x 128 would leave most CUs idle).
+hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st) {
+  if ((epi != EPI_STORE && epi != EPI_RESID) || nsplit < 2 || !a.ws || a.rowscale || a.c_plane || a.c2_plane ||
+      a.K % nsplit || (int64_t)nsplit * a.M * a.N > a.ws_cap || a.N % 4)
+    return hipErrorInvalidValue;
+  GemmArgs b = a;
+  b.k_split = a.K / nsplit;
+  b.C = a.ws;
+  b.ldc = a.N;
+  b.bias = nullptr;
+  b.R = nullptr;
+  b.C2 = nullptr;
+  hipError_t e = gemm_x3(b, EPI_STORE, variant, st);
+  if (e != hipSuccess) return e;
+  GemmArgs c = a;
+  c.k_split = a.K / nsplit;
+  const int64_t n4 = (int64_t)a.M * (a.N / 4);
+  if (epi == EPI_RESID)
+    hipLaunchKernelGGL((splitk_epilogue_kernel<EPI_RESID, false>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, c, nsplit);
+  else
+    hipLaunchKernelGGL((splitk_epilogue_kernel<EPI_STORE, false>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, c, nsplit);
+  return hipGetLastError();
+}
+
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   const int bk = bf16 ? 64 : 32;
   if (bf16 && a.a_bf16) {
@@ -1027,6 +1053,9 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
     if (epi == EPI_GLU && a.N % 128 == 0) return gemm_x3(a, epi, 1, st);
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N >= 1024 && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
+    if ((epi == EPI_STORE || epi == EPI_RESID) && !a.rowscale && a.K >= 1536 && a.M <= 1536 && a.N % 64 == 0 && a.ws &&
+        2ll * a.M * a.N <= a.ws_cap)
+      return gemm_x3_splitk(a, epi, 0, 2, st);   // few tiles, long K (FFN down in the reduced layers)
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_x3(a, epi, 0, st);
   }
   if (!bf16 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {

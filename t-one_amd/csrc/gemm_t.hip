@@ -693,7 +693,11 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
     m0 = (wgid / ntn) * BMX;
     n0 = (wgid % ntn) * BNW;
   }
-  const int nk = p.K / (32 * WK);
+  // split-K (GemmArgs::k_split > 0): this workgroup's K range is [y * k_split, (y + 1) * k_split),
+  // its raw partial goes to slab y of C ([nsplit][M][ldc])
+  const int kofs = p.k_split ? (int)blockIdx.y * p.k_split : 0;
+  if (p.k_split) p.C = static_cast<float*>(p.C) + (int64_t)blockIdx.y * p.M * p.ldc;
+  const int nk = (p.k_split ? p.k_split : p.K) / (32 * WK);
   const float* __restrict__ X = static_cast<const float*>(p.A);
   const uint16_t* __restrict__ X3 = static_cast<const uint16_t*>(p.A);
   const uint16_t* __restrict__ W3 = p.W3;
@@ -709,7 +713,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
     for (int i = 0; i < IPW; ++i) {
       const int piece = wid + i * NW;                           // wave-uniform
       const int g = piece / (WPC + XPC), pr = piece % (WPC + XPC);
-      const int kb = (kt * WK + g) * 32;
+      const int kb = kofs + (kt * WK + g) * 32;
       const void* src;
       float* dst;
       if (pr < WPC) {                                           // 16 W rows x 64 B of plane pl
@@ -886,14 +890,14 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
 
 template <class TL, int EPI>
 hipError_t launch_x3(const GemmArgs& a, hipStream_t st) {
-  const int tiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
+  const dim3 tiles((a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX), a.k_split ? a.K / a.k_split : 1);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
   if (a.a_plane) {
-    if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, true>), dim3(tiles), block, 0, st, a);
-    else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, true>), dim3(tiles), block, 0, st, a);
+    if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, true>), tiles, block, 0, st, a);
+    else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, true>), tiles, block, 0, st, a);
   } else {
-    if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, false>), dim3(tiles), block, 0, st, a);
-    else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, false>), dim3(tiles), block, 0, st, a);
+    if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, false>), tiles, block, 0, st, a);
+    else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, false>), tiles, block, 0, st, a);
   }
   return hipGetLastError();
 }
@@ -902,7 +906,7 @@ template <class TL>
 hipError_t launch_x3_epi(const GemmArgs& a, int epi, hipStream_t st) {
   if (!a.W3 || a.a_bf16 || a.c_bf16 || a.rpg || a.M <= 0 || a.N % TL::BNW || a.K % (32 * TL::WK) || a.lda % 8 ||
       a.ldc % 8 || (a.c_plane && (a.c_plane % 8 || (epi != EPI_SWIGLU && epi != EPI_GLU))) || a.c2_plane % 8 ||
-      a.a_plane % 8)
+      a.a_plane % 8 || (a.k_split && (a.K % a.k_split || a.k_split % (32 * TL::WK) || a.rowscale || epi != EPI_STORE)))
     return hipErrorInvalidValue;
   constexpr bool pairable = (TL::BNW / TL::WN / 32) % 2 == 0;   // g/u 32-row blocks in one wave tile
   switch (epi) {

@@ -195,6 +195,7 @@ int main(int argc, char** argv) {
     auto launch = [&]() {
       return v < 0 ? gemm(a, epi, !f32, 0)
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
+             : (v >= 50 && nsplit > 1) ? gemm_x3_splitk(a, epi, v - 50, nsplit, 0)
              : v >= 50 ? gemm_x3(a, epi, v - 50, 0)
              : v >= 40 ? gemm_f32t(a, epi, v - 40, 0)
              : v >= 30 ? gemm_f32t(a, epi, v - 30, 0)
