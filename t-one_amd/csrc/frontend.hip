@@ -6,6 +6,11 @@
 
 namespace tone {
 
+__device__ __forceinline__ void barrier_lds_c2() {   // keeps LDS-DMA in flight (no vmcnt(0) fence)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 // ---------------------------------------------------------------------------------------------
 // a1.  Tone.forward_for_export raw branch (tone/nn/model.py:164-165) and the streaming concat of
 // FilterbankFeatures.forward_streaming (tone/nn/modules/feats.py:128-133):
@@ -46,8 +51,6 @@ hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, h
 // from x1 in LDS.
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-constexpr int kK1 = kSub1Kt * kSub1Kf;      // 231
-constexpr int kK1P = 256;                   // padded K
 constexpr int kPos1 = kMelT * kSub1F;       // 1320
 
 // ---- fp32 (exact-fp32 MFMA v_mfma_f32_32x32x2_f32): 8 waves per stream, 32-position tiles; the tap
@@ -248,6 +251,152 @@ hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, 
     hipLaunchKernelGGL(sub1_f32_kernel, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w, w1, scale1, shift1,
                        static_cast<float*>(x2));
   }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// a3 conv2 (Conv2d 32->64, k 11x11, stride (3,1)) + BN + SiLU in bf16 mode, one workgroup per stream.
+// The stream's whole channels-last input [38][44][32] (107 KB bf16) is staged in LDS once by LDS-DMA
+// and every one of the 121 taps reads it from there (the implicit GEMM over all streams gathers each
+// input row from L2 once per tap instead).  The 64 x 32 weights of the taps (4 KB each) stream
+// through a 3-slot LDS ring of 4 taps per slot, two slots ahead (one barrier per 4 taps).  MFMA 16x16x32: A = the tap's weights (rows = output channels),
+// B = the slab (columns = output positions p = 34 t + f, input position (3t + kt) * 44 + f + kf), so
+// a lane ends up with 4 consecutive channels of one position: 8-byte bf16 stores into the flat
+// [B*10][34*64] output the subsampling Linear reads.  8 waves: wave w owns position tiles
+// {w, w + 8, w + 16} (22 tiles of 16 cover the 340 positions) x the 4 channel tiles.
+// LDS 16-byte slots are swizzled slot ^ ((q >> 2) & 1) << 1 on the 64-byte rows of both images
+// (q = slab position or weight row), which makes the 16x16x32 fragment reads conflict-free
+// (ds_read_b128 lane groups {0-3,12-15,20-27}, ...): applied to the DMA source, undone on the read.
+constexpr int kC2Pos = kT * kSub2F;                       // 340 output positions per stream
+constexpr int kC2In = kSub2In * kSub1F;                   // 1672 input positions (64 B each)
+constexpr int kC2SlabPieces = (kC2In * 64 + 1023) / 1024; // 105 one-KiB DMA pieces
+constexpr int kC2Taps = kSub2Kt * kSub2Kf;                // 121
+constexpr int kC2Slab = kC2SlabPieces * 1024 / 4;         // floats of the slab image
+constexpr int kC2TP = 4;                                  // taps per ring slot (one barrier per 4 taps)
+constexpr int kC2Ring = 1024 * kC2TP;                     // floats per weight-ring slot (16 KB)
+constexpr int kC2Stages = (kC2Taps + kC2TP - 1) / kC2TP;  // 31
+
+__device__ __forceinline__ int c2_swz(int q) { return ((q >> 2) & 1) << 1; }
+
+__global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restrict__ x2, const uint16_t* __restrict__ w2c,
+                                                         const float* __restrict__ scale, const float* __restrict__ shift,
+                                                         uint16_t* __restrict__ flat) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  // ONE LDS object: slab | 3 ring slots | scale | shift
+  __shared__ __attribute__((aligned(16))) float lds[kC2Slab + 3 * kC2Ring + 2 * kSub2C];
+  float* ring = lds + kC2Slab;
+  float* sc = ring + 3 * kC2Ring;
+  float* sh = sc + kSub2C;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint16_t* xb = x2 + (int64_t)b * kC2In * kSub1C;
+  if (tid < kSub2C) {
+    sc[tid] = scale[tid];
+    sh[tid] = shift[tid];
+  }
+  __syncthreads();                                        // before any LDS-DMA is in flight
+
+  auto stage_taps = [&](int sg) {                         // taps 4 sg .. 4 sg + 3: 16 pieces, 2 per wave
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pc = wid * 2 + h, tap = min(sg * kC2TP + (pc >> 2), kC2Taps);   // past the end: the zero tap
+      const int L = (pc & 3) * 64 + lane, c = L >> 2, s = L & 3;
+      const uint16_t* src = w2c + (int64_t)c * kConv2KPad + tap * kSub1C + ((s ^ c2_swz(c)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, ring + (sg % 3) * kC2Ring + pc * 256, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+  for (int pc = wid; pc < kC2SlabPieces; pc += 8) {       // the stream's input, once
+    const int L = pc * 64 + lane, q = min(L >> 2, kC2In - 1), s = L & 3;
+    const uint16_t* src = xb + q * kSub1C + ((s ^ c2_swz(q)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src, lds + pc * 256, 16, 0, 0);
+#else
+    (void)src;
+#endif
+  }
+  stage_taps(0);
+  stage_taps(1);
+
+  // per position tile: the lane's output position and its input base position
+  const int n = lane & 15, g = lane >> 4;
+  int qb[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int p = min((wid + 8 * i) * 16 + n, kC2Pos - 1);
+    qb[i] = (kSub2Stride * (p / kSub2F)) * kSub1F + p % kSub2F;
+  }
+  const int ntile = wid < 6 ? 3 : 2;                      // 22 tiles over 8 waves (wave-uniform)
+  f32x4 acc[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int sg = 0; sg < kC2Stages; ++sg) {
+    if (sg + 1 < kC2Stages) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds_c2();                                      // stage sg (and the slab) landed; slot (sg+2)%3 free
+    if (sg + 2 < kC2Stages) stage_taps(sg + 2);
+    const float* wst = ring + (sg % 3) * kC2Ring;
+    const int ntap = min(kC2TP, kC2Taps - sg * kC2TP);     // uniform
+#pragma unroll
+    for (int u = 0; u < kC2TP; ++u) {
+      if (u >= ntap) break;
+      const int j = sg * kC2TP + u;
+      const float* wr = wst + u * 1024;
+      const int kt = j / kSub2Kf, kf = j % kSub2Kf, toff = kt * kSub1F + kf;
+      bf16x8 wf[4], xf[3];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int row = 16 * c + n;
+        wf[c] = *reinterpret_cast<const bf16x8*>(wr + row * 16 + ((g ^ c2_swz(row)) << 2));
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int q = qb[i] + toff;
+        xf[i] = *reinterpret_cast<const bf16x8*>(lds + q * 16 + ((g ^ c2_swz(q)) << 2));
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (i < ntile) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], xf[i], acc[i][c], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // epilogue: D[channel][position]; lane: position 16 tile + n, channels 16 c + 4 g + r
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= ntile) break;
+    const int p = (wid + 8 * i) * 16 + n;
+    if (p >= kC2Pos) continue;
+    uint16_t* dst = flat + ((int64_t)b * kC2Pos + p) * kSub2C;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float y[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ch = 16 * c + 4 * g + r;
+        const float z = fmaf(acc[i][c][r], sc[ch], sh[ch]);   // SiLU via v_exp_f32 / v_rcp_f32 (bf16 output)
+        y[r] = z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
+      }
+      const __bf16 h0 = (__bf16)y[0], h1 = (__bf16)y[1], h2 = (__bf16)y[2], h3 = (__bf16)y[3];
+      const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+      const uint32_t hi = (uint32_t)__builtin_bit_cast(uint16_t, h2) | ((uint32_t)__builtin_bit_cast(uint16_t, h3) << 16);
+      *reinterpret_cast<uint2*>(dst + 16 * c + 4 * g) = make_uint2(lo, hi);
+    }
+  }
+}
+
+hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale, const float* shift, void* flat, int B,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(conv2_bf16_kernel, dim3(B), dim3(512), 0, st, static_cast<const uint16_t*>(x2),
+                     static_cast<const uint16_t*>(w2c), scale, shift, static_cast<uint16_t*>(flat));
   return hipGetLastError();
 }
 

@@ -1087,6 +1087,7 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
 
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
                       bool bf16, hipStream_t st) {
+  if (bf16) return launch_conv2_bf16(x2, w, scale, shift, flat, B, st);   // per-stream LDS slab (frontend.hip)
   GemmArgs a{};
   a.A = x2;
   a.W = w;

@@ -64,6 +64,11 @@ hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, h
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
                       bool bf16, hipStream_t st);
 
+// a3 conv2 in bf16 mode, one workgroup per stream over an LDS-resident input slab (frontend.hip);
+// x2 bf16 [B][38][44][32], w2c bf16 [64][3904] tap-major, flat bf16 [B*10][34*64]
+hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale, const float* shift, void* flat, int B,
+                             hipStream_t st);
+
 // a2 log-mel on the fp32 MFMA: power spectrum GEMM over overlapping windows, then filterbank GEMM
 // with the log / fp16 epilogue.  wave [B][2480] fp32 (from launch_mel_prep).
 hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank_p, float* power, float* feats, int B,

@@ -287,6 +287,30 @@ def test_bf16_mode_close_to_oracle(weights, oracle):
     assert np.mean(agree) > 0.97, agree
 
 
+def test_bf16_pre_encode_stage(weights, oracle):
+    """bf16 front end + subsampling (sub1 Toeplitz MFMA, conv2 LDS-slab kernel, Linear, out_norm) vs the
+    oracle's pre-encode output from a carried state: relative L2 error at bf16 level."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    s = ToneSession(weights, precision="bf16", max_batch=4)
+    rng = np.random.default_rng(23)
+    b = 3
+    _, st0 = oracle.step(synthetic_pcm(rng, b, 0.0), None)
+    pcm = synthetic_pcm(rng, b, 0.0)
+    trace = []
+    oracle.step(pcm, st0, trace=trace)
+    try:
+        s.debug_stop(1)
+        gpu_step(s, pcm, st0)
+        got = s.debug_read("rA", (b, 10, C.D_MODEL))
+    finally:
+        s.debug_stop(-1)
+        s.close()
+    ref = trace[1]
+    rel = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+    assert rel < 2e-2, rel
+
+
 def test_bf16_large_batch_paths(weights, oracle):
     """bf16 at a batch large enough for the persistent / two-workgroup GEMM paths (M = 20480 rows):
     a sample of the streams against the oracle, same bounds as the small-batch bf16 check."""
