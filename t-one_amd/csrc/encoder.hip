@@ -249,44 +249,45 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
 // ConformerConvolution depthwise part (conformer_blocks.py:427-433, submodules.py:364-402):
 //   x = [conv state (30) ; g (T)] per channel; next state = x[-30:]
 //   out[t] = SiLU(BN(bias + sum_k w[k] x[t+k]))  with BN folded into (w, b) on the host.
-// One 384-thread workgroup (a thread per channel) handles kDwStreams streams with the channel's 31 taps
-// (stored tap-major) in registers.  Each stream's 23 KB conv-state section is moved HBM<->LDS in 16-byte
-// vectors: state rows are only 2-byte aligned, so the section is read from the enclosing 16-byte-aligned
-// window (the section is interior to the row) and the two partial end vectors are written element-wise.
-constexpr int kDwStreams = 2;
+// A workgroup of CPW threads (a thread per channel) handles NS streams x CPW channels, the channel's 31
+// taps (stored tap-major) in registers: 384 x 2 streams at large batch, 128 x 1 at small batch (B = 256:
+// 768 workgroups instead of 128).  Each stream's slice of the 23 KB conv-state section (CPW x 30 halves)
+// is moved HBM<->LDS in 16-byte vectors: state rows are only 2-byte aligned, so the slice is read from
+// the enclosing 16-byte-aligned window and the two partial end vectors are written element-wise.
 constexpr int kDwSec = kD * kConvS;          // 11520 halves per (stream, layer)
-constexpr int kDwVec = kDwSec / 8 + 1;       // 16-byte vectors covering a misaligned section
-template <int T, bool OBF>
-__global__ void __launch_bounds__(kD) dwconv_kernel(const float* __restrict__ g, StateRef s, int layer,
-                                                    const float* __restrict__ w, const float* __restrict__ bias,
-                                                    void* __restrict__ out, int B) {
-  __shared__ uint4 lds[kDwStreams][kDwVec];
-  const int c = threadIdx.x;
-  int shift[kDwStreams], nvec[kDwStreams];
-  int64_t base[kDwStreams];
+template <int T, bool OBF, int CPW, int NS>
+__global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g, StateRef s, int layer,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     void* __restrict__ out, int B) {
+  constexpr int kSec = CPW * kConvS;           // halves of this workgroup's slice
+  constexpr int kVec = kSec / 8 + 1;           // 16-byte vectors covering a misaligned slice
+  __shared__ uint4 lds[NS][kVec];
+  const int c = threadIdx.x, ch0 = blockIdx.y * CPW, ch = ch0 + c;
+  int shift[NS], nvec[NS];
+  int64_t base[NS];
 #pragma unroll
-  for (int si = 0; si < kDwStreams; ++si) {
-    const int b = min(blockIdx.x * kDwStreams + si, B - 1);
-    base[si] = s.row(b) + kOffConv + (int64_t)layer * kDwSec;
+  for (int si = 0; si < NS; ++si) {
+    const int b = min(blockIdx.x * NS + si, B - 1);
+    base[si] = s.row(b) + kOffConv + (int64_t)layer * kDwSec + ch0 * kConvS;
     const uintptr_t a = reinterpret_cast<uintptr_t>(s.in + base[si]);
     shift[si] = (int)((a & 15) >> 1);
-    nvec[si] = (shift[si] + kDwSec + 7) >> 3;
+    nvec[si] = (shift[si] + kSec + 7) >> 3;
     const uint4* q = reinterpret_cast<const uint4*>(a & ~uintptr_t(15));
-    for (int v = c; v < nvec[si]; v += kD) lds[si][v] = q[v];
+    for (int v = c; v < nvec[si]; v += CPW) lds[si][v] = q[v];
   }
   float wr[kConvK];
 #pragma unroll
-  for (int k = 0; k < kConvK; ++k) wr[k] = w[k * kD + c];
-  const float bb = bias[c];
+  for (int k = 0; k < kConvK; ++k) wr[k] = w[k * kD + ch];
+  const float bb = bias[ch];
   __syncthreads();
 #pragma unroll
-  for (int si = 0; si < kDwStreams; ++si) {
-    const int b = blockIdx.x * kDwStreams + si;
+  for (int si = 0; si < NS; ++si) {
+    const int b = blockIdx.x * NS + si;
     if (b >= B) break;
     __half* h = reinterpret_cast<__half*>(lds[si]) + shift[si] + c * kConvS;
     float x[kConvS + T];
 #pragma unroll
-    for (int t = 0; t < T; ++t) x[kConvS + t] = g[((int64_t)b * T + t) * kD + c];
+    for (int t = 0; t < T; ++t) x[kConvS + t] = g[((int64_t)b * T + t) * kD + ch];
 #pragma unroll
     for (int i = 0; i < kConvS; ++i) x[i] = __half2float(h[i]);
 #pragma unroll
@@ -294,15 +295,15 @@ __global__ void __launch_bounds__(kD) dwconv_kernel(const float* __restrict__ g,
       float acc = bb;
 #pragma unroll
       for (int k = 0; k < kConvK; ++k) acc = fmaf(wr[k], x[t + k], acc);
-      store_act<OBF>(out, ((int64_t)b * T + t) * kD + c, silu_f(acc));
+      store_act<OBF>(out, ((int64_t)b * T + t) * kD + ch, silu_f(acc));
     }
 #pragma unroll
     for (int i = 0; i < kConvS; ++i) h[i] = __float2half_rn(x[T + i]);
   }
   __syncthreads();
 #pragma unroll
-  for (int si = 0; si < kDwStreams; ++si) {
-    const int b = blockIdx.x * kDwStreams + si;
+  for (int si = 0; si < NS; ++si) {
+    const int b = blockIdx.x * NS + si;
     if (b >= B) break;
     const uintptr_t a = reinterpret_cast<uintptr_t>(s.out + base[si]);
     const int sh = (int)((a & 15) >> 1);
@@ -311,29 +312,37 @@ __global__ void __launch_bounds__(kD) dwconv_kernel(const float* __restrict__ g,
     if (sh == shift[si]) {
       uint4* q = reinterpret_cast<uint4*>(a & ~uintptr_t(15));
       const int n = nvec[si];
-      for (int v = c; v < n; v += kD) {
-        if ((v == 0 && sh) || (v == n - 1 && ((sh + kDwSec) & 7))) {
+      for (int v = c; v < n; v += CPW) {
+        if ((v == 0 && sh) || (v == n - 1 && ((sh + kSec) & 7))) {
           const int e0 = v * 8 - sh;
-          for (int e = max(e0, 0); e < min(e0 + 8, kDwSec); ++e) dst[e] = src[e];
+          for (int e = max(e0, 0); e < min(e0 + 8, kSec); ++e) dst[e] = src[e];
         } else {
           q[v] = lds[si][v];
         }
       }
     } else {  // output slab aligned differently from the input slab
-      for (int e = c; e < kDwSec; e += kD) dst[e] = src[e];
+      for (int e = c; e < kSec; e += CPW) dst[e] = src[e];
     }
   }
 }
 
+template <int T, bool OBF>
+static hipError_t launch_dwconv_t(const float* g, StateRef s, int layer, const float* w, const float* b, void* out,
+                                  int B, hipStream_t st) {
+  if (B >= 1024)
+    hipLaunchKernelGGL((dwconv_kernel<T, OBF, kD, 2>), dim3((B + 1) / 2, 1), dim3(kD), 0, st, g, s, layer, w, b, out, B);
+  else
+    hipLaunchKernelGGL((dwconv_kernel<T, OBF, 128, 1>), dim3(B, kD / 128), dim3(128), 0, st, g, s, layer, w, b, out, B);
+  return hipGetLastError();
+}
+
 hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
                          int T, int B, hipStream_t st) {
-  const dim3 grid((B + kDwStreams - 1) / kDwStreams), block(kD);
-  if (T == kT && obf) hipLaunchKernelGGL((dwconv_kernel<kT, true>), grid, block, 0, st, g, s, layer, w, b, out, B);
-  else if (T == kT) hipLaunchKernelGGL((dwconv_kernel<kT, false>), grid, block, 0, st, g, s, layer, w, b, out, B);
-  else if (T == kT / 2 && obf) hipLaunchKernelGGL((dwconv_kernel<kT / 2, true>), grid, block, 0, st, g, s, layer, w, b, out, B);
-  else if (T == kT / 2) hipLaunchKernelGGL((dwconv_kernel<kT / 2, false>), grid, block, 0, st, g, s, layer, w, b, out, B);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (T == kT) return obf ? launch_dwconv_t<kT, true>(g, s, layer, w, b, out, B, st)
+                          : launch_dwconv_t<kT, false>(g, s, layer, w, b, out, B, st);
+  if (T == kT / 2) return obf ? launch_dwconv_t<kT / 2, true>(g, s, layer, w, b, out, B, st)
+                              : launch_dwconv_t<kT / 2, false>(g, s, layer, w, b, out, B, st);
+  return hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------------------------
