@@ -940,6 +940,8 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
   // 8 waves of 32x64 per 128x128 tile once there is a tile per CU (tools/gemm_bench sweep)
   if (t128 >= kTarget / 2) return launch_glds_epi<Tile<128, 128, 4, 2>>(a, epi, 1, st);
+  // half-chip M (the reduced layers at B = 2048): 64x128 LDS-DMA tiles (scripts/bf16_resid_sweep.sh)
+  if ((epi == EPI_STORE || epi == EPI_RESID) && t64 >= kTarget / 2) return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, 1, st);
   if ((epi == EPI_STORE || epi == EPI_RESID) && t64 < kTarget && a.N % 64 == 0 && a.ldc % 8 == 0 && a.lda % 8 == 0 &&
       !a.rpg)
     return gemm_f32t(a, epi, 2, st);   // 64x64 tiles (bf16 operands) instead of a split-K workspace round trip
