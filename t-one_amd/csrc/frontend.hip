@@ -276,7 +276,7 @@ constexpr int kC2TP = 4;                                  // taps per ring slot 
 constexpr int kC2Ring = 1024 * kC2TP;                     // floats per weight-ring slot (16 KB)
 constexpr int kC2Stages = (kC2Taps + kC2TP - 1) / kC2TP;  // 31
 
-__device__ __forceinline__ int c2_swz(int q) { return ((q >> 2) & 1) << 1; }
+__host__ __device__ __forceinline__ int c2_swz(int q) { return ((q >> 2) & 1) << 1; }
 
 __global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restrict__ x2, const uint16_t* __restrict__ w2c,
                                                          const float* __restrict__ scale, const float* __restrict__ shift,
@@ -398,6 +398,171 @@ hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale
   hipLaunchKernelGGL(conv2_bf16_kernel, dim3(B), dim3(512), 0, st, static_cast<const uint16_t*>(x2),
                      static_cast<const uint16_t*>(w2c), scale, shift, static_cast<uint16_t*>(flat));
   return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// a3 conv2 in fp32 (split) mode: the slab kernel above with fp32 arithmetic done as exact 3-way bf16
+// splits (6 products per multiply-add; gemm_t.hip split3 explains the error bound).
+// Workgroup = (stream, half): output rows 5h .. 5h + 4 read input rows 15h .. 15h + 22, an fp32
+// slab of 1012 positions x 128 B (127 KiB) staged once by LDS-DMA.  The weights arrive pre-split and
+// pre-swizzled, one tap (3 planes x 64 channels x 32 bf16 = 12 KiB) per ring slot, double-buffered.
+// K order inside a tap is permuted so that a lane's 8 k-values are the 16-byte slab slots g and
+// g + 4 (channels 4g..4g+3 and 16+4g..16+4g+3): with the slab slot swizzle s ^ ((q >> 1) & 7) the
+// two ds_read_b128 of a 16-position tile are conflict-free for row-aligned tiles.  X is split in
+// registers (split3); 11 tiles of 16 positions cover the 170 positions.
+constexpr int kC3Rows = 5;                                        // output rows per workgroup
+constexpr int kC3InRows = kSub2Stride * (kC3Rows - 1) + kSub2Kt;  // 23
+constexpr int kC3In = kC3InRows * kSub1F;                         // 1012 input positions
+constexpr int kC3SlabPieces = (kC3In * 128 + 1023) / 1024;        // 127
+constexpr int kC3Slab = kC3SlabPieces * 256;                      // floats
+constexpr int kC3Tap = 3 * kSub2C * kSub1C / 2;                   // floats of one tap's planes (12 KiB)
+constexpr int kC3Pos = kC3Rows * kSub2F;                          // 170
+constexpr int kC3Tiles = (kC3Pos + 15) / 16;                      // 11
+static_assert(kC3Slab * 4 + 2 * kC3Tap * 4 + 2 * kSub2C * 4 <= 160 * 1024, "conv2_x3 LDS");
+
+__global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2x,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       float* __restrict__ flat) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float lds[kC3Slab + 2 * kC3Tap + 2 * kSub2C];   // slab | ring | sc | sh
+  float* ring = lds + kC3Slab;
+  float* sc = ring + 2 * kC3Tap;
+  float* sh = sc + kSub2C;
+  const int b = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* xb = x2 + ((int64_t)b * kSub2In * kSub1F + half * kSub2Stride * kC3Rows * kSub1F) * kSub1C;
+  if (tid < kSub2C) {
+    sc[tid] = scale[tid];
+    sh[tid] = shift[tid];
+  }
+  __syncthreads();                                        // before any LDS-DMA is in flight
+
+  auto stage_tap = [&](int j) {                           // 12 one-KiB pieces, contiguous in w2x
+    for (int pc = wid; pc < 12; pc += 8) {
+      const uint16_t* src = w2x + (int64_t)j * (2 * kC3Tap) + pc * 512 + lane * 8;
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, ring + (j & 1) * kC3Tap + pc * 256, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+  for (int pc = wid; pc < kC3SlabPieces; pc += 8) {       // the slab, once: lane -> (q, swizzled slot)
+    const int L = pc * 64 + lane, q = L >> 3, s = (L & 7) ^ ((q >> 1) & 7);
+    const float* src = xb + min(q, kC3In - 1) * kSub1C + s * 4;
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src, lds + pc * 256, 16, 0, 0);
+#else
+    (void)src;
+#endif
+  }
+  stage_tap(0);
+
+  // wave w: position tiles w and w + 8 (when < 11) x all 4 channel tiles, so each slab fragment is
+  // split once per wave and feeds 24 MFMAs (the split VALU, 4 cycles per wave64 op, would otherwise
+  // bound the kernel); per SIMD (waves w, w + 4) 3/3/3/2 tiles
+  const int n = lane & 15, g = lane >> 4;
+  const int ntile = wid < kC3Tiles - 8 ? 2 : 1;           // wave-uniform
+  int qb[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = min((wid + 8 * k) * 16 + n, kC3Pos - 1);
+    qb[k] = kSub2Stride * (p / kSub2F) * kSub1F + p % kSub2F;
+  }
+  int wofs[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int wrow = 16 * ct + n;
+    wofs[ct] = wrow * 16 + ((g ^ c2_swz(wrow)) << 2);
+  }
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[k][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int j = 0; j < kC2Taps; ++j) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds_c2();                                     // tap j (and the slab) landed; slot (j+1)&1 free
+    if (j + 1 < kC2Taps) stage_tap(j + 1);
+    const float* wr = ring + (j & 1) * kC3Tap;
+    bf16x8 w[3][4];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) w[pl][ct] = *reinterpret_cast<const bf16x8*>(wr + pl * 1024 + wofs[ct]);
+    const int kt = j / kSub2Kf, kf = j - kt * kSub2Kf, toff = kt * kSub1F + kf;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < ntile) {
+        const int q = qb[k] + toff, h = (q >> 1) & 7;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(lds + q * 32 + ((g ^ h) << 2));
+        const f32x4 c = *reinterpret_cast<const f32x4*>(lds + q * 32 + (((g + 4) ^ h) << 2));
+        bf16x8 x0, x1, xl;
+        const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const __bf16 h0 = (__bf16)x[e];
+          const float r1 = x[e] - (float)h0;
+          const __bf16 h1 = (__bf16)r1;
+          x0[e] = h0;
+          x1[e] = h1;
+          xl[e] = (__bf16)(r1 - (float)h1);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          f32x4 t = acc[k][ct];
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2][ct], x0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1][ct], x1, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], xl, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1][ct], x0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], x1, t, 0, 0, 0);
+          acc[k][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], x0, t, 0, 0, 0);
+        }
+      }
+    }
+  }
+  // epilogue: D[channel][position]; lane: position tile 16 + n, channels 16 ct + 4 g + r
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (k >= ntile) break;
+    const int p = (wid + 8 * k) * 16 + n;
+    if (p >= kC3Pos) continue;
+    float* dst = flat + ((int64_t)b * kC2Pos + half * kC3Pos + p) * kSub2C;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int ch = 16 * ct + 4 * g;
+      float4 y;
+      y.x = silu_f(fmaf(acc[k][ct][0], sc[ch], sh[ch]));
+      y.y = silu_f(fmaf(acc[k][ct][1], sc[ch + 1], sh[ch + 1]));
+      y.z = silu_f(fmaf(acc[k][ct][2], sc[ch + 2], sh[ch + 2]));
+      y.w = silu_f(fmaf(acc[k][ct][3], sc[ch + 3], sh[ch + 3]));
+      *reinterpret_cast<float4*>(dst + ch) = y;
+    }
+  }
+}
+
+hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, const float* shift, void* flat, int B,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(conv2_x3_kernel, dim3(2 * B), dim3(512), 0, st, static_cast<const float*>(x2),
+                     static_cast<const uint16_t*>(w2x), scale, shift, static_cast<float*>(flat));
+  return hipGetLastError();
+}
+
+// Host-side layout of w2x: [tap][plane][c 64][32 bf16], the k order of a row permuted (k' = 8g + e
+// holds input channel 4g + e for e < 4, 16 + 4g + e - 4 otherwise) and its 16-byte slots swizzled
+// (slot g stored at g ^ c2_swz(c)).  planes[pl][c][tap][ci] are the three bf16 split terms.
+void conv2_x3_pack(const uint16_t* planes, uint16_t* w2x) {
+  for (int tap = 0; tap < kC2Taps; ++tap)
+    for (int pl = 0; pl < 3; ++pl)
+      for (int c = 0; c < kSub2C; ++c)
+        for (int kk = 0; kk < kSub1C; ++kk) {
+          const int g = kk >> 3, e = kk & 7, ci = e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4);
+          const int slot = g ^ c2_swz(c);
+          w2x[(((int64_t)tap * 3 + pl) * kSub2C + c) * kSub1C + slot * 8 + e] =
+              planes[(((int64_t)pl * kSub2C + c) * kC2Taps + tap) * kSub1C + ci];
+        }
 }
 
 }  // namespace tone

@@ -1088,8 +1088,9 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
 }
 
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st) {
+                      bool bf16, hipStream_t st, const void* w2x) {
   if (bf16) return launch_conv2_bf16(x2, w, scale, shift, flat, B, st);   // per-stream LDS slab (frontend.hip)
+  if (w2x) return launch_conv2_x3(x2, w2x, scale, shift, flat, B, st);    // fp32 split mode (frontend.hip)
   GemmArgs a{};
   a.A = x2;
   a.W = w;

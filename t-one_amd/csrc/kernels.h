@@ -62,12 +62,18 @@ hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, h
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,
 // epilogue SiLU(acc*scale + shift) -> flat [B*10][34*64] (f-major, channel-minor).
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st);
+                      bool bf16, hipStream_t st, const void* w2x = nullptr);
 
 // a3 conv2 in bf16 mode, one workgroup per stream over an LDS-resident input slab (frontend.hip);
 // x2 bf16 [B][38][44][32], w2c bf16 [64][3904] tap-major, flat bf16 [B*10][34*64]
 hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale, const float* shift, void* flat, int B,
                              hipStream_t st);
+// a3 conv2 in fp32 (split) mode: two workgroups per stream over fp32 LDS slabs, exact 3-way bf16
+// splits on the bf16 MFMA (frontend.hip); x2 fp32 [B][38][44][32], flat fp32 [B*10][34*64]
+hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, const float* shift, void* flat, int B,
+                           hipStream_t st);
+// host: pack the split planes [3][64][121][32] (bf16 bits) into the conv2_x3 tap-major layout
+void conv2_x3_pack(const uint16_t* planes, uint16_t* w2x);
 
 // a2 log-mel on the fp32 MFMA: power spectrum GEMM over overlapping windows, then filterbank GEMM
 // with the log / fp16 epilogue.  wave [B][2480] fp32 (from launch_mel_prep).

@@ -84,6 +84,7 @@ struct tone_session {
   float *pre_norm, *w1, *scale1, *shift1, *scale2, *shift2, *out_norm;
   void* w1t = nullptr;   // bf16 mode: conv1 weights [kt 11][c 32][kf 32] (kf >= 21 zero)
   void* w2c;
+  uint16_t* w2x = nullptr;   // fp32 (split) mode: conv2 split planes packed for conv2_x3 (frontend.hip)
   void* wsub_out;
   float *wred, *bred, *bred_pw;
   void* wred_pw;
@@ -355,7 +356,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   LAUNCH("mel", mel_gemms(s->wave, s->basis_p, s->fbank_p, s->power, s->feats, B, st));
   if (s->debug_stop == 0) return TONE_OK;
   LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B, st));
-  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st));
+  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, s->w2x));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * kT, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
   LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, shA, 0, st));
@@ -531,6 +532,21 @@ int finalize_weights(tone_session* s) {
       for (int ci = 0; ci < 32; ++ci)
         for (int k = 0; k < 121; ++k) w2r[(size_t)c2 * kw + k * 32 + ci] = (*c2w)[((size_t)c2 * 32 + ci) * 121 + k];
     CALL(upload_w(s, &s->w2c, w2r));
+    if (s->precision == TONE_PRECISION_FP32) {
+      std::vector<uint16_t> pl((size_t)3 * w2r.size()), px(pl.size());
+      const size_t n = w2r.size();
+      for (size_t i = 0; i < n; ++i) {
+        const uint16_t h = f2bf(w2r[i]);
+        const float r1 = w2r[i] - bf2f(h);
+        const uint16_t m = f2bf(r1);
+        pl[i] = h;
+        pl[n + i] = m;
+        pl[2 * n + i] = f2bf(r1 - bf2f(m));
+      }
+      conv2_x3_pack(pl.data(), px.data());
+      CALL(dalloc(s, &s->w2x, px.size()));
+      HIP_TRY(hipMemcpy(s->w2x, px.data(), px.size() * 2, hipMemcpyHostToDevice));
+    }
     CALL(upload(s, &s->scale2, sc));
     CALL(upload(s, &s->shift2, sh));
   }

@@ -331,3 +331,33 @@ def test_bf16_large_batch_paths(weights, oracle):
     s.close()
     assert worst < 0.25, worst
     assert np.mean(agree) > 0.97, agree
+
+
+@pytest.mark.gpu
+def test_fp32_pre_encode_split_vs_mfma(weights, oracle):
+    """fp32 front end + subsampling from a carried state, split mode (conv2 on the two-slab
+    conv2_x3 kernel, 6 bf16 products per MAC) and exact-fp32-MFMA mode (implicit GEMM) vs the
+    oracle's pre-encode output: both at fp32 level, the split no worse than 2x the fp32 MFMA."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    rng = np.random.default_rng(29)
+    b = 5
+    _, st0 = oracle.step(synthetic_pcm(rng, b, 0.0), None)
+    pcm = synthetic_pcm(rng, b, 0.0)
+    trace = []
+    oracle.step(pcm, st0, trace=trace)
+    ref = trace[1]
+    rel = {}
+    for prec in ("fp32", "fp32-mfma"):
+        s = ToneSession(weights, precision=prec, max_batch=8)
+        try:
+            s.debug_stop(1)
+            gpu_step(s, pcm, st0)
+            got = s.debug_read("rA", (b, 10, C.D_MODEL))
+        finally:
+            s.debug_stop(-1)
+            s.close()
+        rel[prec] = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+    print("pre-encode relative L2 error:", rel)
+    assert rel["fp32"] < 1e-4, rel
+    assert rel["fp32"] <= 2 * rel["fp32-mfma"] + 1e-6, rel
