@@ -3,6 +3,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace tone {
 
 constexpr float kInvSqrtD = 0.05103103630798288f;   // 384^-0.5 (submodules.py:51)
@@ -250,8 +252,9 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
 //   x = [conv state (30) ; g (T)] per channel; next state = x[-30:]
 //   out[t] = SiLU(BN(bias + sum_k w[k] x[t+k]))  with BN folded into (w, b) on the host.
 // A workgroup of CPW threads (a thread per channel) handles NS streams x CPW channels, the channel's 31
-// taps (stored tap-major) in registers: 384 x 2 streams at large batch, 128 x 1 at small batch (B = 256:
-// 768 workgroups instead of 128).  Each stream's slice of the 23 KB conv-state section (CPW x 30 halves)
+// taps (stored tap-major) in registers: 192 x 1 stream at large batch, 128 x 1 at small batch (B = 256:
+// 768 workgroups instead of 128); the shapes measure within 1.5 % of each other once the new frames
+// are loaded ahead of the state barrier (profiles/r01_dwconv_sweep.txt).  Each stream's slice of the 23 KB conv-state section (CPW x 30 halves)
 // is moved HBM<->LDS in 16-byte vectors: state rows are only 2-byte aligned, so the slice is read from
 // the enclosing 16-byte-aligned window and the two partial end vectors are written element-wise.
 constexpr int kDwSec = kD * kConvS;          // 11520 halves per (stream, layer)
@@ -279,6 +282,13 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
 #pragma unroll
   for (int k = 0; k < kConvK; ++k) wr[k] = w[k * kD + ch];
   const float bb = bias[ch];
+  float gx[NS][T];   // the new frames, loaded under the state copy's latency
+#pragma unroll
+  for (int si = 0; si < NS; ++si) {
+    const int b = min(blockIdx.x * NS + si, B - 1);
+#pragma unroll
+    for (int t = 0; t < T; ++t) gx[si][t] = g[((int64_t)b * T + t) * kD + ch];
+  }
   __syncthreads();
 #pragma unroll
   for (int si = 0; si < NS; ++si) {
@@ -287,7 +297,7 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
     __half* h = reinterpret_cast<__half*>(lds[si]) + shift[si] + c * kConvS;
     float x[kConvS + T];
 #pragma unroll
-    for (int t = 0; t < T; ++t) x[kConvS + t] = g[((int64_t)b * T + t) * kD + ch];
+    for (int t = 0; t < T; ++t) x[kConvS + t] = gx[si][t];
 #pragma unroll
     for (int i = 0; i < kConvS; ++i) x[i] = __half2float(h[i]);
 #pragma unroll
@@ -329,8 +339,17 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
 template <int T, bool OBF>
 static hipError_t launch_dwconv_t(const float* g, StateRef s, int layer, const float* w, const float* b, void* out,
                                   int B, hipStream_t st) {
-  if (B >= 1024)
+  static const int forced = [] {   // TONE_DWCONV_VARIANT (sweeps only): 0 = 384x2, 1 = 128x1, 2 = 384x1, 3 = 192x1
+    const char* e = std::getenv("TONE_DWCONV_VARIANT");
+    return e ? std::atoi(e) : -1;
+  }();
+  const int v = forced >= 0 ? forced : (B >= 1024 ? 3 : 1);   // profiles/r01_dwconv_sweep.txt
+  if (v == 0)
     hipLaunchKernelGGL((dwconv_kernel<T, OBF, kD, 2>), dim3((B + 1) / 2, 1), dim3(kD), 0, st, g, s, layer, w, b, out, B);
+  else if (v == 2)
+    hipLaunchKernelGGL((dwconv_kernel<T, OBF, kD, 1>), dim3(B, 1), dim3(kD), 0, st, g, s, layer, w, b, out, B);
+  else if (v == 3)
+    hipLaunchKernelGGL((dwconv_kernel<T, OBF, 192, 1>), dim3(B, 2), dim3(192), 0, st, g, s, layer, w, b, out, B);
   else
     hipLaunchKernelGGL((dwconv_kernel<T, OBF, 128, 1>), dim3(B, kD / 128), dim3(128), 0, st, g, s, layer, w, b, out, B);
   return hipGetLastError();
