@@ -1055,9 +1055,12 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
     if (epi == EPI_GLU && a.N % 128 == 0) return gemm_x3(a, epi, 1, st);
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N >= 1024 && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
-    if ((epi == EPI_STORE || epi == EPI_RESID) && !a.rowscale && a.K >= 1536 && a.M <= 1536 && a.N % 64 == 0 && a.ws &&
-        2ll * a.M * a.N <= a.ws_cap)
-      return gemm_x3_splitk(a, epi, 0, 2, st);   // few tiles, long K (FFN down in the reduced layers)
+    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0 && a.K % 128 == 0 &&
+        (int64_t)((a.M + 63) / 64) * (a.N / 64) <= 160)
+      // few 64x64 tiles (the reduced layers at B = 256, M = 1280): 32x64 tiles with a four-way in-WG
+      // K split fill twice the CUs; beats split-K on FFN down (19.1 vs 22.2 us) and the 64x64 tile on the
+      // K = 384 projections (8.1 vs 11.1 us) (scripts/x3n_sweep.sh, profiles/r01_x3n_sweep_b256.jsonl)
+      return gemm_x3(a, epi, 10, st);
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_x3(a, epi, 0, st);
   }
   if (!bf16 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {

@@ -1051,6 +1051,10 @@ hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     case 6: return launch_x3_epi<XT<128, 128, 2, 4, 1, 3>>(a, epi, st);   // 8 waves, 120 KiB
     case 7: return launch_x3_epi<XT<256, 128, 4, 2, 1, 2>>(a, epi, st);   // 8 waves, 128 KiB
     case 8: return launch_x3_epi<XT<128, 256, 2, 4, 1, 2>>(a, epi, st);   // 8 waves, 112 KiB
+    // narrow tiles, four-way in-workgroup K split: twice the workgroups for the N = 384 projections
+    case 9: return launch_x3_epi<XT<64, 32, 2, 1, 4, 2>>(a, epi, st);     // 8 waves, 128 KiB
+    case 10: return launch_x3_epi<XT<32, 64, 1, 2, 4, 2>>(a, epi, st);    // 8 waves, 112 KiB
+    case 11: return launch_x3_epi<XT<64, 32, 2, 1, 2, 3>>(a, epi, st);    // 4 waves, 96 KiB
     default: return hipErrorInvalidValue;
   }
 }

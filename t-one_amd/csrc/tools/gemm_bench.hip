@@ -184,9 +184,9 @@ int main(int argc, char** argv) {
     a.dbg = (fl >> 2) & 7;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
-    const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 40) || (v >= 50 && v < 70);
+    const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 40) || (v >= 50 && v < 90);
     // -2: gemm() fp32 routing with W planes, -3: without, -4: with W and A planes
-    a.W3 = (vv == -2 || vv == -4 || (v >= 50 && v < 70)) ? W3 : nullptr;
+    a.W3 = (vv == -2 || vv == -4 || (v >= 50 && v < 90)) ? W3 : nullptr;
     a.a_plane = (vv == -4 || (v >= 60 && v < 70)) ? (int64_t)M * K : 0;
     a.A = a.a_plane ? (const void*)A3 : f32 ? (const void*)Af : (const void*)A;
     a.W = f32 ? (const void*)Wf : (const void*)W;
@@ -194,6 +194,7 @@ int main(int argc, char** argv) {
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
       return v < 0 ? gemm(a, epi, !f32, 0)
+             : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
              : (v >= 50 && nsplit > 1) ? gemm_x3_splitk(a, epi, v - 50, nsplit, 0)
              : v >= 50 ? gemm_x3(a, epi, v - 50, 0)
