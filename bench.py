@@ -276,6 +276,7 @@ def main() -> None:
         }
         print(json.dumps(out), flush=True)
     if pg is not None:
+        pg.barrier()   # rank 0 finishes its roofline pass before any rank tears the communicator down
         pg.destroy_process_group()
 
 
