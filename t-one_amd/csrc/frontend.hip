@@ -2,6 +2,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace tone {
@@ -420,7 +421,8 @@ constexpr int kC3Pos = kC3Rows * kSub2F;                          // 170
 constexpr int kC3Tiles = (kC3Pos + 15) / 16;                      // 11
 static_assert(kC3Slab * 4 + 2 * kC3Tap * 4 + 2 * kSub2C * 4 <= 160 * 1024, "conv2_x3 LDS");
 
-__global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2x,
+template <int NWV>   // waves per workgroup (8: two per SIMD; 4: one per SIMD, 3 tiles each)
+__global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2x,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        float* __restrict__ flat) {
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -439,7 +441,7 @@ __global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__
   __syncthreads();                                        // before any LDS-DMA is in flight
 
   auto stage_tap = [&](int j) {                           // 12 one-KiB pieces, contiguous in w2x
-    for (int pc = wid; pc < 12; pc += 8) {
+    for (int pc = wid; pc < 12; pc += NWV) {
       const uint16_t* src = w2x + (int64_t)j * (2 * kC3Tap) + pc * 512 + lane * 8;
 #if defined(__HIP_DEVICE_COMPILE__)
       __builtin_amdgcn_global_load_lds(src, ring + (j & 1) * kC3Tap + pc * 256, 16, 0, 0);
@@ -448,7 +450,7 @@ __global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__
 #endif
     }
   };
-  for (int pc = wid; pc < kC3SlabPieces; pc += 8) {       // the slab, once: lane -> (q, swizzled slot)
+  for (int pc = wid; pc < kC3SlabPieces; pc += NWV) {     // the slab, once: lane -> (q, swizzled slot)
     const int L = pc * 64 + lane, q = L >> 3, s = (L & 7) ^ ((q >> 1) & 7);
     const float* src = xb + min(q, kC3In - 1) * kSub1C + s * 4;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -462,12 +464,13 @@ __global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__
   // wave w: position tiles w and w + 8 (when < 11) x all 4 channel tiles, so each slab fragment is
   // split once per wave and feeds 24 MFMAs (the split VALU, 4 cycles per wave64 op, would otherwise
   // bound the kernel); per SIMD (waves w, w + 4) 3/3/3/2 tiles
+  constexpr int KT = (kC3Tiles + NWV - 1) / NWV, KU = kC3Tiles / NWV;   // tiles per wave: max, unconditional
   const int n = lane & 15, g = lane >> 4;
-  const int ntile = wid < kC3Tiles - 8 ? 2 : 1;           // wave-uniform
-  int qb[2];
+  const int ntile = wid + NWV * (KT - 1) < kC3Tiles ? KT : KT - 1;   // wave-uniform
+  int qb[KT];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int p = min((wid + 8 * k) * 16 + n, kC3Pos - 1);
+  for (int k = 0; k < KT; ++k) {
+    const int p = min((wid + NWV * k) * 16 + n, kC3Pos - 1);
     qb[k] = kSub2Stride * (p / kSub2F) * kSub1F + p % kSub2F;
   }
   int wofs[4];
@@ -476,9 +479,9 @@ __global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__
     const int wrow = 16 * ct + n;
     wofs[ct] = wrow * 16 + ((g ^ c2_swz(wrow)) << 2);
   }
-  f32x4 acc[2][4];
+  f32x4 acc[KT][4];
 #pragma unroll
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < KT; ++k)
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc[k][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -494,8 +497,8 @@ __global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__
       for (int ct = 0; ct < 4; ++ct) w[pl][ct] = *reinterpret_cast<const bf16x8*>(wr + pl * 1024 + wofs[ct]);
     const int kt = j / kSub2Kf, kf = j - kt * kSub2Kf, toff = kt * kSub1F + kf;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k < ntile) {
+    for (int k = 0; k < KT; ++k) {
+      if (k < KU || k < ntile) {
         const int q = qb[k] + toff, h = (q >> 1) & 7;
         const f32x4 a = *reinterpret_cast<const f32x4*>(lds + q * 32 + ((g ^ h) << 2));
         const f32x4 c = *reinterpret_cast<const f32x4*>(lds + q * 32 + (((g + 4) ^ h) << 2));
@@ -525,9 +528,9 @@ __global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__
   }
   // epilogue: D[channel][position]; lane: position tile 16 + n, channels 16 ct + 4 g + r
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < KT; ++k) {
     if (k >= ntile) break;
-    const int p = (wid + 8 * k) * 16 + n;
+    const int p = (wid + NWV * k) * 16 + n;
     if (p >= kC3Pos) continue;
     float* dst = flat + ((int64_t)b * kC2Pos + half * kC3Pos + p) * kSub2C;
 #pragma unroll
@@ -545,8 +548,16 @@ __global__ void __launch_bounds__(512) conv2_x3_kernel(const float* __restrict__
 
 hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, const float* shift, void* flat, int B,
                            hipStream_t st) {
-  hipLaunchKernelGGL(conv2_x3_kernel, dim3(2 * B), dim3(512), 0, st, static_cast<const float*>(x2),
-                     static_cast<const uint16_t*>(w2x), scale, shift, static_cast<float*>(flat));
+  static const int nwv = [] {   // TONE_CONV2_WAVES (sweeps only): 8 (default) or 4
+    const char* e = std::getenv("TONE_CONV2_WAVES");
+    return e ? std::atoi(e) : 8;
+  }();
+  if (nwv == 4)
+    hipLaunchKernelGGL(conv2_x3_kernel<4>, dim3(2 * B), dim3(256), 0, st, static_cast<const float*>(x2),
+                       static_cast<const uint16_t*>(w2x), scale, shift, static_cast<float*>(flat));
+  else
+    hipLaunchKernelGGL(conv2_x3_kernel<8>, dim3(2 * B), dim3(512), 0, st, static_cast<const float*>(x2),
+                       static_cast<const uint16_t*>(w2x), scale, shift, static_cast<float*>(flat));
   return hipGetLastError();
 }
 
