@@ -155,14 +155,15 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
   // 8 shifted copies, each padded by 32 B so the copies start 8 banks apart (a wave's A reads hit
   // all 8 copies at the same in-copy offset)
   constexpr int kCopy = kRows * kX1Cols + 16;
+  // LDS kept under 80 KiB so two streams share a CU: the sub2 state goes HBM -> x2 and tile -> HBM
+  // directly (no [c][8][44] staging copy), and x1 is dead once the shifted copies exist
   __shared__ __attribute__((aligned(16))) uint16_t xc[8 * kCopy];
-  __shared__ float x1[kRows * kMels];
+  __shared__ __attribute__((aligned(16))) float x1[kRows * kMels];   // later: per-wave output tiles
   __shared__ float sc[kSub1C], sh[kSub1C];
-  __shared__ __half st2[kSub1C * kSub2S * kSub1F];      // sub2 state [c][8][44]: carried in, then next
-  __shared__ __attribute__((aligned(16))) uint16_t tbuf[8][16 * kSub1C];   // per-wave output tile (16 pos x 32 ch)
+  uint16_t(*tbuf)[16 * kSub1C] = reinterpret_cast<uint16_t(*)[16 * kSub1C]>(x1);   // 8 x 1 KiB <= 10 KiB
+  static_assert(8 * 16 * kSub1C * 2 <= kRows * kMels * 4, "tbuf fits in x1");
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t srow = s.row(b);
-  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) st2[i] = s.in[srow + kOffSub2 + i];
   // weight fragments: B operand lane (n = lane & 15, k group g = lane >> 4): w1t[kt][16 nt + n][8 g .. 8 g + 7]
   const int g = lane >> 4, n = lane & 15;
   bf16x8 wf[kSub1Kt][2];
@@ -183,13 +184,14 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
   }
   uint16_t* xb = x2 + (int64_t)b * kSub2In * kSub1F * kSub1C;
   __syncthreads();
+  const __half* st2in = s.in + srow + kOffSub2;          // sub2 state [c][8][44]
   for (int i = tid; i < kSub1C * kSub2S * kSub1F / 8; i += 512) {   // carried rows -> x2 rows 0..7 (channels-last)
     const int c = (8 * i) % kSub1C, rf = (8 * i) / kSub1C;            // 8 channels per thread, 16-byte stores
     uint32_t w[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const __bf16 lo = (__bf16)__half2float(st2[(c + 2 * q) * kSub2S * kSub1F + rf]);
-      const __bf16 hi = (__bf16)__half2float(st2[(c + 2 * q + 1) * kSub2S * kSub1F + rf]);
+      const __bf16 lo = (__bf16)__half2float(st2in[(c + 2 * q) * kSub2S * kSub1F + rf]);
+      const __bf16 hi = (__bf16)__half2float(st2in[(c + 2 * q + 1) * kSub2S * kSub1F + rf]);
       w[q] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
     }
     *reinterpret_cast<uint4*>(xb + 8 * i) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -200,7 +202,8 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
     const __bf16 h = (__bf16)v;
     xc[sh8 * kCopy + r * kX1Cols + j] = __builtin_bit_cast(uint16_t, h);
   }
-  __syncthreads();
+  __syncthreads();                                        // x1 is dead from here: its space holds tbuf
+  __half* st2out = s.out + srow + kOffSub2;
   for (int tile = wid; tile < kMelT * 3; tile += 8) {
     const int t = tile / 3, f0 = (tile % 3) * 16;
     const int a = f0 + n + 8 * g, sh8 = a & 7;                 // A operand: position f0 + n, k group g
@@ -226,7 +229,7 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
         const float y = z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
         const __bf16 hy = (__bf16)y;
         tw[(4 * g + r) * kSub1C + c] = __builtin_bit_cast(uint16_t, hy);
-        if (f < kSub1F && t >= kMelT - kSub2S) st2[(c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
+        if (f < kSub1F && t >= kMelT - kSub2S) st2out[(c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -238,8 +241,6 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
-  __syncthreads();
-  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) s.out[srow + kOffSub2 + i] = st2[i];
 }
 
 hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
