@@ -84,6 +84,27 @@ __device__ __forceinline__ void store_act(void* base, int64_t i, float v) {
     static_cast<float*>(base)[i] = v;
   }
 }
+// activation loads matching store_act: element i of an fp32 or bf16 (OBF) array; four consecutive
+// elements (16-byte / 8-byte aligned)
+template <bool OBF>
+__device__ __forceinline__ float load_act(const void* base, int64_t i) {
+  if constexpr (OBF) {
+    const uint32_t u = (uint32_t) static_cast<const uint16_t*>(base)[i] << 16;
+    return __builtin_bit_cast(float, u);
+  } else {
+    return static_cast<const float*>(base)[i];
+  }
+}
+template <bool OBF>
+__device__ __forceinline__ float4 load_act4(const void* base, int64_t i) {
+  if constexpr (OBF) {
+    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(base) + i);
+    return make_float4(__builtin_bit_cast(float, u.x << 16), __builtin_bit_cast(float, u.x & 0xffff0000u),
+                       __builtin_bit_cast(float, u.y << 16), __builtin_bit_cast(float, u.y & 0xffff0000u));
+  } else {
+    return *reinterpret_cast<const float4*>(static_cast<const float*>(base) + i);
+  }
+}
 __device__ __forceinline__ void store_bf16(uint16_t* base, int64_t i, float v) {
   __bf16 h = (__bf16)v;
   base[i] = __builtin_bit_cast(uint16_t, h);

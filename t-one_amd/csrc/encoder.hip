@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
   const int cl = min(lane, kDk - 1);
   float vr[TK];                               // V column cl, all keys (issued first: in flight meanwhile)
 #pragma unroll
-  for (int j = 0; j < TK; ++j) vr[j] = a.v[((int64_t)b * TK + j) * a.ldv + c0 + cl];
+  for (int j = 0; j < TK; ++j) vr[j] = load_act<OBF>(a.v, ((int64_t)b * TK + j) * a.ldv + c0 + cl);
   if constexpr (REC) {
     // LayerNorm + RoPE of one 48-dim row held in registers; pos = RoPE position
     auto ln_rope = [&](float (&x)[kDk], const float* lw, const float* lb, int pos) {
@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
       float qr[kDk];
 #pragma unroll
       for (int c4 = 0; c4 < kDk / 4; ++c4) {
-        const float4 v = *reinterpret_cast<const float4*>(a.q + ((int64_t)b * T + lane) * a.ldq + c0 + 4 * c4);
+        const float4 v = load_act4<OBF>(a.q, ((int64_t)b * T + lane) * a.ldq + c0 + 4 * c4);
         qr[4 * c4] = v.x; qr[4 * c4 + 1] = v.y; qr[4 * c4 + 2] = v.z; qr[4 * c4 + 3] = v.w;
       }
       ln_rope(qr, a.qln_w, a.qln_b, lane);
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
     const int jr = min(lane, TK - 1);
 #pragma unroll
     for (int c4 = 0; c4 < kDk / 4; ++c4) {
-      const float4 v = *reinterpret_cast<const float4*>(a.k + ((int64_t)b * TK + jr) * a.ldk + c0 + 4 * c4);
+      const float4 v = load_act4<OBF>(a.k, ((int64_t)b * TK + jr) * a.ldk + c0 + 4 * c4);
       kr[4 * c4] = v.x; kr[4 * c4 + 1] = v.y; kr[4 * c4 + 2] = v.z; kr[4 * c4 + 3] = v.w;
     }
     ln_rope(kr, a.kln_w, a.kln_b, jr - S);

@@ -99,9 +99,9 @@ hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, i
                               void* xn, void* kv, bool obf, int B, hipStream_t st);
 
 struct AttnArgs {
-  const float* q; int64_t ldq;      // rows b*T+i
-  const float* k; int64_t ldk;      // rows b*(S+T)+j
-  const float* v; int64_t ldv;      // rows b*(S+T)+j
+  const void* q; int64_t ldq;       // rows b*T+i; fp32, or bf16 bits when ctx_bf16 (bf16 mode)
+  const void* k; int64_t ldk;       // rows b*(S+T)+j, same type
+  const void* v; int64_t ldv;       // rows b*(S+T)+j, same type
   void* ctx;                        // [B*T][384], fp32 or bf16 (ctx_bf16)
   float* probs;                     // [B][8][T][S+T]: written when scores are computed, read when shared
   const float* qln_w; const float* qln_b; const float* kln_w; const float* kln_b;

@@ -344,6 +344,11 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
     if (_rc) return _rc; \
   } while (0)
 
+// element `i` of an activation buffer held as fp32, or as bf16 bits in bf16 mode
+const void* act_at(const float* base, int64_t i, bool bf) {
+  return bf ? static_cast<const void*>(reinterpret_cast<const uint16_t*>(base) + i) : static_cast<const void*>(base + i);
+}
+
 // The whole streaming step (Tone.forward_for_export, model.py:162-205).
 // bf16 mode: every GEMM operand is bf16 in memory -- the residual keeps an fp32 master copy plus a
 // bf16 shadow written by each of its producers; the other operands are produced in bf16 directly.
@@ -390,30 +395,33 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     if (l < 14) {
       const bool rec = (l == 0 || l == 7);
       const int N = rec ? 3 * D : D;
-      CALL(gemm_call(s, st, "gemm_qkv", xa, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1, nullptr, 1.0f, true));
+      // q/k/v in bf16 in bf16 mode (half the attention kernel's input bytes)
+      CALL(gemm_call(s, st, "gemm_qkv", xa, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1, nullptr, 1.0f, true,
+                     bf));
       aa.S = 0;
       aa.recompute = rec;
       aa.reduced = 0;
       if (rec) {
-        aa.q = s->qkv; aa.ldq = N;
-        aa.k = s->qkv + D; aa.ldk = N;
-        aa.v = s->qkv + 2 * D; aa.ldv = N;
+        aa.q = act_at(s->qkv, 0, bf); aa.ldq = N;
+        aa.k = act_at(s->qkv, D, bf); aa.ldk = N;
+        aa.v = act_at(s->qkv, 2 * D, bf); aa.ldv = N;
       } else {
         aa.v = s->qkv; aa.ldv = D;
       }
     } else {
       const int S = (l == 14) ? kMhsaS / 2 : kMhsaS;
       LAUNCH("kv_assemble", launch_kv_assemble(x, w.norm_att, sr, l - 14, T, S, s->xn, s->kv, bf, B, st));
-      CALL(gemm_call(s, st, "gemm_qkv", s->xn, D, w.wq, s->qkv, D, w.bq, M, D, D, EPI_STORE, 0, nullptr, 1.0f, true));
+      CALL(gemm_call(s, st, "gemm_qkv", s->xn, D, w.wq, s->qkv, D, w.bq, M, D, D, EPI_STORE, 0, nullptr, 1.0f, true,
+                     bf));
       CALL(gemm_call(s, st, "gemm_qkv", s->kv, D, w.wkv, s->kvp, 2 * D, w.bkv, B * (S + T), 2 * D, D, EPI_STORE, 0,
-                     nullptr, 1.0f, true));
+                     nullptr, 1.0f, true, bf));
       aa.S = S;
       aa.recompute = 1;
       aa.reduced = (l == 14);
       aa.probs = nullptr;
       aa.q = s->qkv; aa.ldq = D;
-      aa.k = s->kvp; aa.ldk = 2 * D;
-      aa.v = s->kvp + D; aa.ldv = 2 * D;
+      aa.k = act_at(s->kvp, 0, bf); aa.ldk = 2 * D;
+      aa.v = act_at(s->kvp, D, bf); aa.ldv = 2 * D;
     }
     LAUNCH("attention", launch_attention(aa, st));
     CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
