@@ -70,7 +70,9 @@ int tone_session_set_weight(tone_session *s, const char *name, const float *host
 int tone_session_finalize(tone_session *s);
 
 /* Enable (1) / disable (0) hipGraph capture+replay of the per-step kernel sequence, keyed by
- * (batch, I/O pointers).  Default 0. */
+ * (batch, I/O pointers, frame_info pointer, state stride).  At most 16 executable graphs are kept
+ * (least recently used evicted), so callers should reuse fixed I/O buffers.  Runs on the NULL stream,
+ * with timing on, or with a debug stop set are never captured.  Default 0. */
 int tone_session_set_graph(tone_session *s, int enable);
 
 /* Optional per-frame decode outputs of later runs (device pointer, int32 [batch][10], or NULL):
@@ -89,10 +91,22 @@ int tone_session_set_frame_info(tone_session *s, int32_t *frame_info);
 int tone_session_run(tone_session *s, const int32_t *signal, const uint16_t *state_in, float *logprobs,
                      uint16_t *state_out, int batch, int64_t state_stride, void *stream);
 
-/* Same step with the state in a device-resident slab of `n_slots` rows: stream i reads row
- * slots[i] of slab_in and writes row slots[i] of slab_out (slot ids are device int32). */
+/* Same step with the state in a device-resident slab of n_slots rows: stream i reads row
+ * slots[i] of slab_in and writes row slots[i] of slab_out.
+ *   slots       int32  [batch]                device memory; ids distinct and in [0, n_slots) -- the
+ *                                             kernels index the slabs with them unchecked, so the caller
+ *                                             validates (tone_amd.model.ToneSession.run_slots does)
+ *   slab_in/out fp16   [n_slots][slab_stride] slab_stride >= 219729, equal for both, not aliased
+ * Rows of slab_out not named in slots are not written. */
 int tone_session_run_slots(tone_session *s, const int32_t *signal, const int32_t *slots, const uint16_t *slab_in,
                            uint16_t *slab_out, int64_t slab_stride, float *logprobs, int batch, void *stream);
+
+/* Same step over ONE slab whose rows are used in ping-pong: stream i reads row rows_in[i] and writes
+ * row rows_out[i] (device int32 [batch] each).  No row may appear in both lists, and the ids must be
+ * in [0, n_rows) (unchecked, as for run_slots).  A server keeps two rows per stream and flips only the
+ * streams that step, so streams without audio this step keep their state with no copy. */
+int tone_session_run_rows(tone_session *s, const int32_t *signal, const int32_t *rows_in, const int32_t *rows_out,
+                          uint16_t *slab, int64_t slab_stride, float *logprobs, int batch, void *stream);
 
 /* Workspace bytes the session holds on the device (weights + activations). */
 int64_t tone_session_device_bytes(const tone_session *s);

@@ -200,8 +200,12 @@ class StreamState:
 class ToneOracle:
     """One streaming step of the acoustic path, float32 numpy."""
 
-    def __init__(self, weights: dict):
+    def __init__(self, weights: dict, round_feats: bool = True):
+        """``round_feats=False`` skips rounding point #2 (features -> fp16): what
+        ``Tone.forward_for_export`` computes when handed float32 states (its preprocessor then
+        returns float32 features), used to pin the oracle against tests/golden/golden_fx.npz."""
         self.W = {k: np.asarray(v, dtype=F32) for k, v in weights.items()}
+        self.round_feats = round_feats
         self.basis = forward_basis()
         self.fbank = mel_filterbank()
 
@@ -216,8 +220,8 @@ class ToneOracle:
         spec = frames @ self.basis.T                                                # (B, 30, 162)
         power = spec[..., : C.N_BINS] ** 2 + spec[..., C.N_BINS:] ** 2             # (B, 30, 81)
         mel = power @ self.fbank.T                                                  # (B, 30, 64)
-        feats = fp16(np.log(mel + np.float32(C.LOG_GUARD)))
-        return feats, nxt
+        feats = np.log(mel + np.float32(C.LOG_GUARD)).astype(F32)
+        return (fp16(feats) if self.round_feats else feats), nxt
 
     # --- a3: convolutional subsampling (conformer_blocks.py:614-653) ------------------------
     def pre_encode(self, feats: np.ndarray, st: StreamState, nst: dict) -> np.ndarray:

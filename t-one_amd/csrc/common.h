@@ -50,13 +50,19 @@ constexpr float kLnEps = 1e-5f;
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-// Where stream b's state row lives: row b, or row slots[b] of a device-resident slab.
+// Where stream b's state rows live: row b of state_in / state_out, or rows slots[b] of device-resident
+// slabs; with slots_out, stream b reads row slots[b] and writes row slots_out[b] (ping-pong rows of one
+// slab, so streams that sit out a step keep their state without a copy).
 struct StateRef {
   const __half* in;
   __half* out;
   int64_t stride;          // elements between consecutive rows
-  const int* slots;        // nullptr -> identity
-  __device__ __forceinline__ int64_t row(int b) const { return (int64_t)(slots ? slots[b] : b) * stride; }
+  const int* slots;        // rows read (nullptr -> identity)
+  const int* slots_out;    // rows written (nullptr -> the rows read)
+  __device__ __forceinline__ int64_t row_in(int b) const { return (int64_t)(slots ? slots[b] : b) * stride; }
+  __device__ __forceinline__ int64_t row_out(int b) const {
+    return slots_out ? (int64_t)slots_out[b] * stride : row_in(b);
+  }
 };
 
 __device__ __forceinline__ float wave_sum(float v) {

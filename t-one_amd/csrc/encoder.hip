@@ -52,7 +52,8 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
   // copies; ns = 4 at small batch (four workgroups per stream: the copies are latency-bound there; at
   // B = 2048 one workgroup per stream is faster, 85 vs 104 us per step)
   const int b = blockIdx.x, y = blockIdx.y, ns = gridDim.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t cache = s.row(b) + kOffMhsa + (int64_t)layer_slot * kMhsaS * kD;
+  const int64_t sec = kOffMhsa + (int64_t)layer_slot * kMhsaS * kD;
+  const int64_t cache = s.row_in(b) + sec, cache_out = s.row_out(b) + sec;
   const int TK = S + T;
   // normalized current rows
   for (int i = 4 * y + wid; i < T; i += 4 * ns) {
@@ -69,7 +70,7 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
       store_act<OBF>(xn, ((int64_t)b * T + i) * kD + c, y);
       store_act<OBF>(kv, ((int64_t)b * TK + S + i) * kD + c, y);
       // new cache row (30 - S) + (S - T + i) = 30 - T + i holds xn[i]
-      s.out[cache + (int64_t)(kMhsaS - T + i) * kD + c] = __float2half_rn(y);
+      s.out[cache_out + (int64_t)(kMhsaS - T + i) * kD + c] = __float2half_rn(y);
     }
   }
   // cached rows: stored rows 30-S .. 29
@@ -82,7 +83,7 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
     const int rr = i / kD, c = i % kD;
     __half h = __float2half_rn(0.f);
     if (rr >= kMhsaS - S) h = s.in[cache + (int64_t)(rr + T) * kD + c];
-    s.out[cache + (int64_t)rr * kD + c] = h;
+    s.out[cache_out + (int64_t)rr * kD + c] = h;
   }
 }
 
@@ -175,7 +176,7 @@ __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float off = -1e30f;
     if constexpr (S > 0) {
-      off = (float)kMhsaS - __half2float(a.s.in[a.s.row(b) + kOffMhsaLen]);
+      off = (float)kMhsaS - __half2float(a.s.in[a.s.row_in(b) + kOffMhsaLen]);
       if (a.reduced) off = floorf(off / 2.0f);
     }
     const bool live = lane < TK;
@@ -272,10 +273,11 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
   const int c = threadIdx.x, ch0 = blockIdx.y * CPW, ch = ch0 + c;
   int shift[NS], nvec[NS];
   int64_t base[NS];
+  const int64_t sec = kOffConv + (int64_t)layer * kDwSec + ch0 * kConvS;
 #pragma unroll
   for (int si = 0; si < NS; ++si) {
     const int b = min(blockIdx.x * NS + si, B - 1);
-    base[si] = s.row(b) + kOffConv + (int64_t)layer * kDwSec + ch0 * kConvS;
+    base[si] = s.row_in(b) + sec;
     const uintptr_t a = reinterpret_cast<uintptr_t>(s.in + base[si]);
     shift[si] = (int)((a & 15) >> 1);
     nvec[si] = (shift[si] + kSec + 7) >> 3;
@@ -319,9 +321,9 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
   for (int si = 0; si < NS; ++si) {
     const int b = blockIdx.x * NS + si;
     if (b >= B) break;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(s.out + base[si]);
+    __half* dst = s.out + s.row_out(b) + sec;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
     const int sh = (int)((a & 15) >> 1);
-    __half* dst = s.out + base[si];
     const __half* src = reinterpret_cast<const __half*>(lds[si]) + shift[si];
     if (sh == shift[si]) {
       uint4* q = reinterpret_cast<uint4*>(a & ~uintptr_t(15));
@@ -379,11 +381,10 @@ __global__ void __launch_bounds__(256) reduce_conv_kernel(const float* __restric
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= B * kD) return;
   const int b = idx / kD, c = idx % kD;
-  const int64_t srow = s.row(b);
   float xc[kT + 1];
-  xc[0] = __half2float(s.in[srow + kOffRed + c]);
+  xc[0] = __half2float(s.in[s.row_in(b) + kOffRed + c]);
   for (int t = 0; t < kT; ++t) xc[t + 1] = x[((int64_t)b * kT + t) * kD + c];
-  s.out[srow + kOffRed + c] = __float2half_rn(xc[kT]);
+  s.out[s.row_out(b) + kOffRed + c] = __float2half_rn(xc[kT]);
   for (int q = 0; q < 4; ++q) {
     const int o = 4 * c + q;
     const float w0 = w[o * 3], w1 = w[o * 3 + 1], w2 = w[o * 3 + 2], bo = bias[o];

@@ -23,15 +23,15 @@ __global__ void __launch_bounds__(256) mel_prep_kernel(const int32_t* __restrict
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)B * kWave) return;
   const int b = (int)(idx / kWave), i = (int)(idx % kWave);
-  const int64_t srow = s.row(b);
+  const int64_t srow = s.row_in(b), orow = s.row_out(b);
   __half hv;
   if (i < kPreState) hv = s.in[srow + kOffPre + i];
   else hv = __float2half_rn((float)pcm[(int64_t)b * kChunk + (i - kPreState)] / 32767.0f);
   wave[idx] = __half2float(hv);
-  if (i >= kChunk) s.out[srow + kOffPre + (i - kChunk)] = hv;
+  if (i >= kChunk) s.out[orow + kOffPre + (i - kChunk)] = hv;
   if (i == 0) {
     const float ml = __half2float(s.in[srow + kOffMhsaLen]);
-    s.out[srow + kOffMhsaLen] = __float2half_rn(fminf(ml + (float)kT, (float)kMhsaS));
+    s.out[orow + kOffMhsaLen] = __float2half_rn(fminf(ml + (float)kT, (float)kMhsaS));
   }
 }
 
@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
   __shared__ __half st2[kSub1C * kSub2S * kSub1F];      // sub2 state [c][8][44]: carried in, then next
   __shared__ __attribute__((aligned(16))) float tbuf[8][32 * kSub1C];   // per-wave output tile (32 pos x 32 ch)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t srow = s.row(b);
+  const int64_t srow = s.row_in(b), orow = s.row_out(b);
   for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) st2[i] = s.in[srow + kOffSub2 + i];
   for (int i = tid; i < kSub1C * kSub1Kt * kKfP; i += 512) {
     const int c = i / (kSub1Kt * kKfP), k = i % (kSub1Kt * kKfP), kt = k / kKfP, kf = k % kKfP;
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
     const float rms = sqrtf(ssq) * 0.125f;          // * 64^-0.5
     const float y = pre_norm_w[lane] * (v / (rms + kRmsEps));
     x1[(kSub1S + t) * kMels + lane] = y;
-    if (t >= kMelT - kSub1S) s.out[srow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
+    if (t >= kMelT - kSub1S) s.out[orow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
   }
   float* xb = x2 + (int64_t)b * kSub2In * kSub1F * kSub1C;
   __syncthreads();
@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) s.out[srow + kOffSub2 + i] = st2[i];
+  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) s.out[orow + kOffSub2 + i] = st2[i];
 }
 
 // ---- bf16 (v_mfma_f32_16x16x32_bf16): conv1 as a Toeplitz GEMM.  For output row t and kernel row
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
   uint16_t(*tbuf)[16 * kSub1C] = reinterpret_cast<uint16_t(*)[16 * kSub1C]>(x1);   // 8 x 1 KiB <= 10 KiB
   static_assert(8 * 16 * kSub1C * 2 <= kRows * kMels * 4, "tbuf fits in x1");
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t srow = s.row(b);
+  const int64_t srow = s.row_in(b), orow = s.row_out(b);
   // weight fragments: B operand lane (n = lane & 15, k group g = lane >> 4): w1t[kt][16 nt + n][8 g .. 8 g + 7]
   const int g = lane >> 4, n = lane & 15;
   bf16x8 wf[kSub1Kt][2];
@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
     const float rms = sqrtf(ssq) * 0.125f;
     const float y = pre_norm_w[lane] * (v / (rms + kRmsEps));
     x1[(kSub1S + t) * kMels + lane] = y;
-    if (t >= kMelT - kSub1S) s.out[srow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
+    if (t >= kMelT - kSub1S) s.out[orow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
   }
   uint16_t* xb = x2 + (int64_t)b * kSub2In * kSub1F * kSub1C;
   __syncthreads();
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
     xc[sh8 * kCopy + r * kX1Cols + j] = __builtin_bit_cast(uint16_t, h);
   }
   __syncthreads();                                        // x1 is dead from here: its space holds tbuf
-  __half* st2out = s.out + srow + kOffSub2;
+  __half* st2out = s.out + orow + kOffSub2;
   for (int tile = wid; tile < kMelT * 3; tile += 8) {
     const int t = tile / 3, f0 = (tile % 3) * 16;
     const int a = f0 + n + 8 * g, sh8 = a & 7;                 // A operand: position f0 + n, k group g

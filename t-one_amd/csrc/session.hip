@@ -102,13 +102,19 @@ struct tone_session {
   // graphs
   struct GraphKey {
     int batch;
-    const void *a, *b, *c, *d, *e, *f;
+    const void *a, *b, *c, *d, *e, *f, *g;
     int64_t stride;
     bool operator<(const GraphKey& o) const {
       return std::memcmp(this, &o, sizeof(GraphKey)) < 0;
     }
   };
-  std::map<GraphKey, hipGraphExec_t> graphs;
+  struct CachedGraph {
+    hipGraphExec_t exec;
+    uint64_t last_use;
+  };
+  static constexpr size_t kMaxGraphs = 16;
+  std::map<GraphKey, CachedGraph> graphs;
+  uint64_t graph_clock = 0;
 
   // timing
   struct Timed {
@@ -728,10 +734,11 @@ int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp,
     return fail(TONE_E_INVALID, "batch " + std::to_string(batch) + " outside 1.." + std::to_string(s->max_batch));
   if (!signal || !sr.in || !sr.out || !logp) return fail(TONE_E_INVALID, "null I/O pointer");
   if (sr.stride < kStateSize) return fail(TONE_E_INVALID, "state stride < 219729");
-  if (sr.in == sr.out) return fail(TONE_E_INVALID, "state_out must not alias state_in");
+  if (sr.in == sr.out && !sr.slots_out) return fail(TONE_E_INVALID, "state_out must not alias state_in");
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (s->use_graph && st != nullptr && !s->timing) {
+  // graphs replay a captured step keyed by (batch, I/O pointers); debug stops and timing run eagerly
+  if (s->use_graph && st != nullptr && !s->timing && s->debug_stop < 0) {
     tone_session::GraphKey k;
     std::memset(&k, 0, sizeof(k));
     k.batch = batch;
@@ -741,6 +748,7 @@ int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp,
     k.d = logp;
     k.e = sr.slots;
     k.f = s->frame_info;
+    k.g = sr.slots_out;
     k.stride = sr.stride;
     (void)key_a;
     (void)key_b;
@@ -750,14 +758,29 @@ int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp,
       int rc = enqueue_step(s, signal, sr, logp, batch, st);
       hipGraph_t graph = nullptr;
       hipError_t e = hipStreamEndCapture(st, &graph);
-      if (rc) return rc;
-      if (e != hipSuccess) return fail(TONE_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+      if (rc || e != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        if (rc) return rc;
+        return fail(TONE_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+      }
       hipGraphExec_t exec = nullptr;
-      HIP_TRY(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-      HIP_TRY(hipGraphDestroy(graph));
-      it = s->graphs.emplace(k, exec).first;
+      e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      if (e != hipSuccess) return fail(TONE_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+      // bounded cache: a server that keeps changing pointers or batch sizes evicts the least recently
+      // used executable graph instead of growing without limit
+      if (s->graphs.size() >= tone_session::kMaxGraphs) {
+        auto lru = s->graphs.begin();
+        for (auto g = s->graphs.begin(); g != s->graphs.end(); ++g)
+          if (g->second.last_use < lru->second.last_use) lru = g;
+        HIP_TRY(hipStreamSynchronize(st));   // the evicted graph may still be in flight on this stream
+        (void)hipGraphExecDestroy(lru->second.exec);
+        s->graphs.erase(lru);
+      }
+      it = s->graphs.emplace(k, tone_session::CachedGraph{exec, 0}).first;
     }
-    HIP_TRY(hipGraphLaunch(it->second, st));
+    it->second.last_use = ++s->graph_clock;
+    HIP_TRY(hipGraphLaunch(it->second.exec, st));
     return TONE_OK;
   }
   return enqueue_step(s, signal, sr, logp, batch, st);
@@ -792,7 +815,7 @@ int tone_session_create(tone_session** out, int device, int precision, int max_b
 int tone_session_destroy(tone_session* s) {
   if (!s) return TONE_OK;
   (void)hipSetDevice(s->device);
-  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second.exec);
   for (auto& t : s->timed) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
@@ -836,14 +859,24 @@ int tone_session_set_frame_info(tone_session* s, int32_t* frame_info) {
 
 int tone_session_run(tone_session* s, const int32_t* signal, const uint16_t* state_in, float* logprobs,
                      uint16_t* state_out, int batch, int64_t state_stride, void* stream) {
-  StateRef sr{reinterpret_cast<const __half*>(state_in), reinterpret_cast<__half*>(state_out), state_stride, nullptr};
+  StateRef sr{reinterpret_cast<const __half*>(state_in), reinterpret_cast<__half*>(state_out), state_stride, nullptr,
+              nullptr};
   return run_common(s, signal, sr, logprobs, batch, stream, nullptr, nullptr);
 }
 
 int tone_session_run_slots(tone_session* s, const int32_t* signal, const int32_t* slots, const uint16_t* slab_in,
                            uint16_t* slab_out, int64_t slab_stride, float* logprobs, int batch, void* stream) {
   if (!slots) return fail(TONE_E_INVALID, "null slots");
-  StateRef sr{reinterpret_cast<const __half*>(slab_in), reinterpret_cast<__half*>(slab_out), slab_stride, slots};
+  StateRef sr{reinterpret_cast<const __half*>(slab_in), reinterpret_cast<__half*>(slab_out), slab_stride, slots,
+              nullptr};
+  return run_common(s, signal, sr, logprobs, batch, stream, nullptr, nullptr);
+}
+
+int tone_session_run_rows(tone_session* s, const int32_t* signal, const int32_t* rows_in, const int32_t* rows_out,
+                          uint16_t* slab, int64_t slab_stride, float* logprobs, int batch, void* stream) {
+  if (!rows_in || !rows_out) return fail(TONE_E_INVALID, "null rows");
+  if (rows_in == rows_out) return fail(TONE_E_INVALID, "rows_out must differ from rows_in");
+  StateRef sr{reinterpret_cast<const __half*>(slab), reinterpret_cast<__half*>(slab), slab_stride, rows_in, rows_out};
   return run_common(s, signal, sr, logprobs, batch, stream, nullptr, nullptr);
 }
 

@@ -77,14 +77,85 @@ class ToneSession:
                                               state_out.data_ptr(), b, state_in.stride(0), st),
                    "tone_session_run")
 
-    def run_slots(self, signal, slots, slab_in, slab_out, logprobs, stream=None) -> None:
-        """Stream i uses row slots[i] of the device-resident state slabs (int32 slot ids)."""
+    def run_slots(self, signal, slots, slab_in, slab_out, logprobs, stream=None, check_slots: bool = True) -> None:
+        """Stream i reads row slots[i] of ``slab_in`` and writes row slots[i] of ``slab_out``.
+
+        signal int32 (B,2400), slots int32 (B,) on the device (or a host sequence, uploaded here),
+        slab_in/slab_out fp16 (n_slots, >= 219729) with equal row strides, logprobs fp32 (>= B,10,35).
+        Slot ids must be distinct and in [0, n_slots): with ``check_slots`` (default) a device slots
+        tensor is range-checked here (one device sync), a host sequence always is."""
         torch = _torch()
+        b = int(signal.shape[0])
+        if not isinstance(slots, torch.Tensor):
+            ids = [int(x) for x in slots]
+            if len(ids) != b:
+                raise ValueError(f"{len(ids)} slots for a batch of {b}")
+            n = int(slab_in.shape[0])
+            if any(not 0 <= x < n for x in ids) or len(set(ids)) != b:
+                raise ValueError(f"slot ids must be distinct and in [0, {n})")
+            slots = torch.tensor(ids, dtype=torch.int32, device=self.dev)
+            check_slots = False
+        for t, dt in ((signal, torch.int32), (slots, torch.int32), (slab_in, torch.float16),
+                      (slab_out, torch.float16), (logprobs, torch.float32)):
+            if t.dtype != dt or t.device != self.dev:
+                raise ValueError(f"expected {dt} tensor on {self.dev}, got {t.dtype} on {t.device}")
+        if not 0 < b <= self.max_batch:
+            raise ValueError(f"batch {b} outside 1..{self.max_batch}")
+        if tuple(slots.shape) != (b,) or not slots.is_contiguous():
+            raise ValueError(f"slots must be a contiguous (B,) = ({b},) int32 tensor, got {tuple(slots.shape)}")
+        if signal.dim() < 2 or signal.shape[1] != C.AUDIO_CHUNK_SAMPLES or not signal.is_contiguous():
+            raise ValueError(f"signal must be a contiguous (B, {C.AUDIO_CHUNK_SAMPLES}) int32 tensor")
+        if not logprobs.is_contiguous() or logprobs.numel() < b * C.CHUNK_FRAMES * C.VOCAB:
+            raise ValueError("logprobs must be contiguous with room for (B, 10, 35)")
+        if slab_in.dim() != 2 or slab_out.shape != slab_in.shape or slab_in.stride(1) != 1 or slab_out.stride(1) != 1 \
+                or slab_in.stride(0) != slab_out.stride(0) or slab_in.stride(0) < C.STATE_SIZE \
+                or slab_in.shape[1] < C.STATE_SIZE:
+            raise ValueError("slabs must be equal-shaped (n_slots, >= 219729) fp16 with unit column stride and "
+                             "equal row strides")
+        if slab_in.data_ptr() == slab_out.data_ptr():
+            raise ValueError("slab_out must not alias slab_in")
+        if check_slots and b:
+            lo, hi = int(slots.min()), int(slots.max())
+            if lo < 0 or hi >= slab_in.shape[0]:
+                raise ValueError(f"slot ids span [{lo}, {hi}], outside [0, {slab_in.shape[0]})")
         st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
         _lib.check(self._lib.tone_session_run_slots(self._h, signal.data_ptr(), slots.data_ptr(), slab_in.data_ptr(),
-                                                    slab_out.data_ptr(), slab_in.stride(0), logprobs.data_ptr(),
-                                                    int(signal.shape[0]), st),
+                                                    slab_out.data_ptr(), slab_in.stride(0), logprobs.data_ptr(), b, st),
                    "tone_session_run_slots")
+
+    def run_rows(self, signal, rows_in, rows_out, slab, logprobs, stream=None, check_rows: bool = True) -> None:
+        """Ping-pong step over one slab: stream i reads row rows_in[i] and writes row rows_out[i].
+
+        rows_in/rows_out int32 (B,) device tensors; slab fp16 (n_rows, >= 219729).  No row may be both
+        read and written (checked with one device sync when ``check_rows``)."""
+        torch = _torch()
+        b = int(signal.shape[0])
+        for t, dt in ((signal, torch.int32), (rows_in, torch.int32), (rows_out, torch.int32),
+                      (slab, torch.float16), (logprobs, torch.float32)):
+            if t.dtype != dt or t.device != self.dev:
+                raise ValueError(f"expected {dt} tensor on {self.dev}, got {t.dtype} on {t.device}")
+        if not 0 < b <= self.max_batch:
+            raise ValueError(f"batch {b} outside 1..{self.max_batch}")
+        for r in (rows_in, rows_out):
+            if tuple(r.shape) != (b,) or not r.is_contiguous():
+                raise ValueError(f"rows must be contiguous (B,) = ({b},) int32 tensors, got {tuple(r.shape)}")
+        if signal.dim() < 2 or signal.shape[1] != C.AUDIO_CHUNK_SAMPLES or not signal.is_contiguous():
+            raise ValueError(f"signal must be a contiguous (B, {C.AUDIO_CHUNK_SAMPLES}) int32 tensor")
+        if not logprobs.is_contiguous() or logprobs.numel() < b * C.CHUNK_FRAMES * C.VOCAB:
+            raise ValueError("logprobs must be contiguous with room for (B, 10, 35)")
+        if slab.dim() != 2 or slab.stride(1) != 1 or slab.stride(0) < C.STATE_SIZE or slab.shape[1] < C.STATE_SIZE:
+            raise ValueError("slab must be (n_rows, >= 219729) fp16 with unit column stride")
+        if check_rows:
+            both = torch.cat([rows_in, rows_out])
+            lo, hi = int(both.min()), int(both.max())
+            if lo < 0 or hi >= slab.shape[0]:
+                raise ValueError(f"row ids span [{lo}, {hi}], outside [0, {slab.shape[0]})")
+            if int(torch.unique(both).numel()) != 2 * b:
+                raise ValueError("row ids must be distinct: no row both read and written, no row used twice")
+        st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
+        _lib.check(self._lib.tone_session_run_rows(self._h, signal.data_ptr(), rows_in.data_ptr(), rows_out.data_ptr(),
+                                                   slab.data_ptr(), slab.stride(0), logprobs.data_ptr(), b, st),
+                   "tone_session_run_rows")
 
     def set_frame_info(self, frame_info=None) -> None:
         """Have later runs also write frame_info int32 (>= max_batch, 10): greedy token | speech << 8
@@ -159,7 +230,9 @@ def validate_inputs(audio_chunk, state):
         )
     if audio_chunk.dtype != np.int32:
         raise ValueError(f"Incorrect dtype of 'audio_chunk': expected np.int32, but got {audio_chunk.dtype}")
-    if audio_chunk.size and (audio_chunk.min() < -32768 or audio_chunk.max() > 32767):
+    if audio_chunk.size == 0:   # the reference's audio_chunk.min() raises ValueError on it (onnx_wrapper.py:108)
+        raise ValueError("zero-size array to reduction operation minimum which has no identity")
+    if audio_chunk.min() < -32768 or audio_chunk.max() > 32767:
         raise ValueError(
             "Samples in 'audio_chunk' must be in range [-32768; 32767], "
             f"but it is in range [{audio_chunk.min()}; {audio_chunk.max()}]",
@@ -194,30 +267,33 @@ class StreamingCTCModel:
     STATE_SIZE = C.STATE_SIZE
 
     HF_REPO = "t-tech/T-one"
-    HF_WEIGHTS = "model.safetensors"
+    HF_MODEL = "model.onnx"          # what tone/onnx_wrapper.py:60-63 fetches
+    HF_WEIGHTS = "model.safetensors"   # the torch checkpoint of the same model, used when present
 
     @classmethod
-    def from_hugging_face(cls) -> "StreamingCTCModel":
-        """tone/onnx_wrapper.py:38-50 -- resolves the checkpoint through the HF cache."""
-        return cls.from_local(cls.download_from_hugging_face())
+    def from_hugging_face(cls, **kw) -> "StreamingCTCModel":
+        """tone/onnx_wrapper.py:38-50 -- resolves ``model.onnx`` through the HF cache."""
+        return cls.from_local(cls.download_from_hugging_face(), **kw)
 
     @classmethod
     def download_from_hugging_face(cls) -> str:
-        """tone/onnx_wrapper.py:52-63, but fetching the torch checkpoint (this path does not run
-        ONNX graphs).  Works offline when the file is already in the HF cache."""
+        """tone/onnx_wrapper.py:52-63: ``hf_hub_download("t-tech/T-one", "model.onnx")`` (works offline
+        when the file is already in the HF cache)."""
         from huggingface_hub import hf_hub_download
-        return hf_hub_download(cls.HF_REPO, cls.HF_WEIGHTS)
+        return hf_hub_download(cls.HF_REPO, cls.HF_MODEL)
 
     @classmethod
     def from_local(cls, model_path: str | Path, providers: Optional[list[str]] = None, *, device: int = 0,
                    precision: str = "fp32", max_batch: int = 64) -> "StreamingCTCModel":
-        """tone/onnx_wrapper.py:65-78.  ``model_path``: model.safetensors / weights.npz / torch
-        state_dict (.pt, weights_only) or a directory holding one.  ``providers`` is accepted for
-        signature compatibility; the MI355X device is chosen with ``device``."""
+        """tone/onnx_wrapper.py:65-78.  ``model_path`` is what the reference passes -- ``model.onnx``
+        (its initializers are read by :mod:`tone_amd.onnx_weights`; a ``model.safetensors`` beside it
+        is preferred when present) -- or a model.safetensors / weights.npz / torch state_dict (.pt,
+        weights_only) / a directory holding one.  ``providers`` is accepted for signature
+        compatibility; the MI355X device is chosen with ``device``."""
         del providers
         p = Path(model_path)
-        if p.suffix == ".onnx":   # StreamingCTCPipeline.from_local passes dir/model.onnx (pipeline.py:213)
-            p = p.parent
+        if p.suffix == ".onnx" and (p.parent / cls.HF_WEIGHTS).exists():
+            p = p.parent / cls.HF_WEIGHTS
         return cls(ToneSession(load_weights(p), device=device, precision=precision, max_batch=max_batch))
 
     @classmethod
@@ -254,8 +330,6 @@ class StreamingCTCModel:
         batch_size = audio_chunk.shape[0]
 
         torch = _torch()
-        if batch_size == 0:
-            return (np.zeros((0, C.CHUNK_FRAMES, C.VOCAB), np.float32), np.zeros((0, C.STATE_SIZE), np.float16))
         outs_l, outs_s = [], []
         for s0 in range(0, batch_size, self._sess.max_batch):
             s1 = min(batch_size, s0 + self._sess.max_batch)

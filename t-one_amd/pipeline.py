@@ -15,8 +15,14 @@ and the splitter / greedy decoder below run on (token, speech) frames with the r
   * phrase times            pipeline.py:151-168
 
 ``StreamingGreedyPipeline`` serves many concurrent streams from one ``ToneSession``: each stream owns
-a row ("slot") of a device-resident state slab, every step runs the active streams as one batch
-through ``tone_session_run_slots``, and only the frame info crosses PCIe.
+two rows of a device-resident state slab used in ping-pong, every step runs the streams that have
+audio as one batch through ``tone_session_run_rows`` (read one row, write the other; streams without
+audio are not touched, no state is copied), and only the frame info crosses PCIe.
+``StreamScheduler`` puts an arrival queue in front of it (the role Triton's dynamic / sequence
+batcher plays for the reference, configs/streaming_acoustic/config.pbtxt:35-37,
+triton/model/config.pbtxt:26-69): chunks arrive per stream at any time, each step packs up to
+``max_batch`` streams that have a chunk waiting (oldest waiting chunk first, one chunk per stream per
+step so every stream's chunks run in order) into one device batch.
 """
 
 from __future__ import annotations
@@ -118,6 +124,9 @@ class StreamingGreedyPipeline:
     Drop-in counterpart of ``StreamingCTCPipeline(model, StreamingLogprobSplitter(), GreedyCTCDecoder())``
     (tone/pipeline.py) for a server: ``open_stream`` / ``close_stream`` manage slots of the device
     state slab, ``forward`` advances any subset of open streams by one 300 ms chunk each.
+
+    Slot s owns slab rows 2s and 2s+1; ``_parity[s]`` says which one holds its current state.  A
+    step reads row 2s + p and writes row 2s + 1 - p for the stepping streams only.
     """
 
     CHUNK_SIZE = C.AUDIO_CHUNK_SAMPLES
@@ -129,22 +138,27 @@ class StreamingGreedyPipeline:
         self.session = session
         self.n_slots = int(n_slots)
         dev = session.dev
-        # two slabs: a step reads slab[cur] and writes slab[1 - cur] (run_slots must not alias)
-        self._slab = [torch.zeros((self.n_slots, STATE_STRIDE), dtype=torch.float16, device=dev) for _ in range(2)]
-        self._cur = 0
+        self._slab = torch.zeros((2 * self.n_slots, STATE_STRIDE), dtype=torch.float16, device=dev)
+        self._parity = np.zeros(self.n_slots, np.int32)
         self._open: dict[int, FrameSplitterState] = {}
         self._free = list(range(self.n_slots - 1, -1, -1))
         mb = session.max_batch
+        # fixed staging buffers: the device pointers stay the same across steps (hipGraph friendly)
         self._info = torch.zeros((mb, C.CHUNK_FRAMES), dtype=torch.int32, device=dev)
         self._logp = torch.empty((mb, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev)
-        session.set_frame_info(self._info)
+        self._sig = torch.zeros((mb, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32, device=dev)
+        self._rows = torch.zeros((2, mb), dtype=torch.int32, device=dev)
+        self._sig_h = torch.zeros((mb, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32).pin_memory()
+        self._rows_h = torch.zeros((2, mb), dtype=torch.int32).pin_memory()
+        self._info_h = torch.zeros((mb, C.CHUNK_FRAMES), dtype=torch.int32).pin_memory()
 
     # --- slots -------------------------------------------------------------------------------
     def open_stream(self) -> int:
         if not self._free:
             raise RuntimeError(f"all {self.n_slots} stream slots are in use")
         slot = self._free.pop()
-        self._slab[self._cur][slot].zero_()          # onnx_wrapper.py:114-115: zero state at stream start
+        self._parity[slot] = 0
+        self._slab[2 * slot].zero_()          # onnx_wrapper.py:114-115: zero state at stream start
         self._open[slot] = FrameSplitterState()
         return slot
 
@@ -158,11 +172,41 @@ class StreamingGreedyPipeline:
     def open_slots(self) -> list[int]:
         return sorted(self._open)
 
+    def state_of(self, slot: int):
+        """The current flat (219729,) fp16 state of an open stream (a device tensor view)."""
+        if slot not in self._open:
+            raise KeyError(f"slot {slot} is not open")
+        return self._slab[2 * slot + int(self._parity[slot]), : C.STATE_SIZE]
+
     # --- one step ----------------------------------------------------------------------------
+    def step_frames(self, chunks: np.ndarray, slots: Sequence[int]) -> np.ndarray:
+        """Advance ``slots`` by one chunk each on the device; returns their frame info (n, 10) int32."""
+        import torch
+        n = len(slots)
+        mb = self.session.max_batch
+        info = np.empty((n, C.CHUNK_FRAMES), np.int32)
+        self.session.set_frame_info(self._info)    # frame_info is session state: claim it every step
+        for b0 in range(0, n, mb):
+            b1 = min(n, b0 + mb)
+            nb = b1 - b0
+            sl = np.asarray(slots[b0:b1], np.int64)
+            par = self._parity[sl]
+            self._sig_h[:nb].numpy()[:] = chunks[b0:b1]
+            self._rows_h[0, :nb].numpy()[:] = 2 * sl + par
+            self._rows_h[1, :nb].numpy()[:] = 2 * sl + 1 - par
+            self._sig[:nb].copy_(self._sig_h[:nb], non_blocking=True)
+            self._rows[:, :nb].copy_(self._rows_h[:, :nb], non_blocking=True)
+            self.session.run_rows(self._sig[:nb], self._rows[0, :nb], self._rows[1, :nb], self._slab,
+                                  self._logp, check_rows=False)   # rows are built here, distinct by construction
+            self._info_h[:nb].copy_(self._info[:nb], non_blocking=True)
+            torch.cuda.current_stream(self.session.dev).synchronize()
+            info[b0:b1] = self._info_h[:nb].numpy()
+            self._parity[sl] ^= 1
+        return info
+
     def forward(self, chunks: np.ndarray, slots: Sequence[int], is_last: Optional[Sequence[bool]] = None
                 ) -> list[list[TextPhrase]]:
         """chunks int32 (n, 2400) for the open streams ``slots`` -> per stream, the finished phrases."""
-        import torch
         if not isinstance(chunks, np.ndarray):
             raise TypeError(f"Incorrect 'chunks' type: expected np.ndarray, but got {type(chunks)}")
         n = len(slots)
@@ -175,21 +219,8 @@ class StreamingGreedyPipeline:
         if len(set(slots)) != n or any(s not in self._open for s in slots):
             raise ValueError("slots must be distinct open stream slots")
         is_last = [False] * n if is_last is None else list(is_last)
-        src, dst = self._slab[self._cur], self._slab[1 - self._cur]
-        idle = [s for s in self._open if s not in set(slots)]
-        if idle:   # streams without a chunk this step keep their state: carry their rows across
-            idx = torch.tensor(idle, dtype=torch.int64, device=src.device)
-            dst.index_copy_(0, idx, src.index_select(0, idx))
+        info = self.step_frames(chunks, slots) if n else np.zeros((0, C.CHUNK_FRAMES), np.int32)
         out: list[list[TextPhrase]] = []
-        mb = self.session.max_batch
-        info = np.empty((n, C.CHUNK_FRAMES), np.int32)
-        for b0 in range(0, n, mb):
-            b1 = min(n, b0 + mb)
-            sig = torch.from_numpy(np.ascontiguousarray(chunks[b0:b1])).to(src.device)
-            sl = torch.tensor(list(slots[b0:b1]), dtype=torch.int32, device=src.device)
-            self.session.run_slots(sig, sl, src, dst, self._logp[:b1 - b0])
-            info[b0:b1] = self._info[:b1 - b0].cpu().numpy()
-        self._cur ^= 1
         for i, slot in enumerate(slots):
             toks, speech = decode_frame_info(info[i])
             phrases, self._open[slot] = frames_to_phrases(toks, speech, self._open[slot], is_last=is_last[i])
@@ -213,3 +244,72 @@ class StreamingGreedyPipeline:
             return phrases
         finally:
             self.close_stream(slot)
+
+
+class StreamScheduler:
+    """Arrival queue + continuous batching in front of a :class:`StreamingGreedyPipeline`.
+
+    ``submit(stream_id, chunk, is_last)`` may be called at any time for any number of streams (a
+    stream's slot is opened at its first chunk and released after its last).  ``step()`` takes the
+    streams whose oldest waiting chunk arrived first, at most ``max_batch`` of them and one chunk
+    each, runs them as one device batch and returns ``{stream_id: [TextPhrase, ...]}`` for the
+    streams that stepped.  Streams with nothing waiting are not in the batch and their state rows
+    are not touched.
+    """
+
+    def __init__(self, pipeline: StreamingGreedyPipeline, max_batch: Optional[int] = None):
+        from collections import deque
+        self.pipe = pipeline
+        self.max_batch = int(max_batch or pipeline.session.max_batch)
+        if self.max_batch <= 0:
+            raise ValueError("max_batch must be positive")
+        self._queues: dict = {}          # stream id -> deque[(seq, chunk, is_last)]
+        self._slot: dict = {}            # stream id -> slot
+        self._seq = 0
+        self._deque = deque
+
+    def submit(self, stream_id, chunk: np.ndarray, is_last: bool = False) -> None:
+        chunk = np.asarray(chunk)
+        if chunk.shape != (C.AUDIO_CHUNK_SAMPLES,) or chunk.dtype != np.int32:
+            raise ValueError(f"chunk must be int32 ({C.AUDIO_CHUNK_SAMPLES},), got {chunk.dtype} {chunk.shape}")
+        if stream_id not in self._slot:
+            self._slot[stream_id] = self.pipe.open_stream()
+            self._queues[stream_id] = self._deque()
+        q = self._queues[stream_id]
+        if q and q[-1][2]:
+            raise ValueError(f"stream {stream_id!r} already submitted its last chunk")
+        q.append((self._seq, chunk, bool(is_last)))
+        self._seq += 1
+
+    @property
+    def pending(self) -> int:
+        return sum(len(q) for q in self._queues.values())
+
+    @property
+    def active_streams(self) -> int:
+        return len(self._slot)
+
+    def step(self) -> dict:
+        ready = [(q[0][0], sid) for sid, q in self._queues.items() if q]
+        if not ready:
+            return {}
+        ready.sort()
+        pick = [sid for _, sid in ready[: self.max_batch]]
+        items = [self._queues[sid].popleft() for sid in pick]
+        chunks = np.stack([it[1] for it in items])
+        res = self.pipe.forward(chunks, [self._slot[sid] for sid in pick], [it[2] for it in items])
+        out = {}
+        for sid, it, phrases in zip(pick, items, res):
+            out[sid] = phrases
+            if it[2]:
+                self.pipe.close_stream(self._slot.pop(sid))
+                del self._queues[sid]
+        return out
+
+    def drain(self) -> dict:
+        """Step until nothing is waiting; phrases concatenated per stream."""
+        out: dict = {}
+        while self.pending:
+            for sid, ph in self.step().items():
+                out.setdefault(sid, []).extend(ph)
+        return out

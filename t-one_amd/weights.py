@@ -153,17 +153,23 @@ def normalize_keys(sd: dict) -> "OrderedDict[str, np.ndarray]":
 
 
 def load_weights(path: str | Path) -> "OrderedDict[str, np.ndarray]":
-    """Load weights from ``model.safetensors`` / ``*.npz`` / ``*.pt`` (weights_only) or a dir.
+    """Load weights from ``model.safetensors`` / ``*.npz`` / ``*.pt`` (weights_only) /
+    ``model.onnx`` (graph initializers, :mod:`tone_amd.onnx_weights`) or a directory holding one.
 
     Only loaders that execute nothing from the file are used (safetensors, numpy without
     pickle, ``torch.load(weights_only=True)``).
     """
     p = Path(path)
     if p.is_dir():
-        for cand in ("model.safetensors", "weights.npz", "pytorch_model.bin"):
+        for cand in ("model.safetensors", "weights.npz", "pytorch_model.bin", "model.onnx"):
             if (p / cand).exists():
                 return load_weights(p / cand)
-        raise FileNotFoundError(f"no model.safetensors / weights.npz / pytorch_model.bin in {p}")
+        raise FileNotFoundError(f"no model.safetensors / weights.npz / pytorch_model.bin / model.onnx in {p}")
+    if not p.exists():
+        raise FileNotFoundError(f"weight file {p} does not exist")
+    if p.suffix == ".onnx":
+        from .onnx_weights import load_onnx_weights
+        return load_onnx_weights(p)
     if p.suffix == ".safetensors":
         from safetensors.numpy import load_file
         return normalize_keys(load_file(str(p)))
@@ -173,4 +179,4 @@ def load_weights(path: str | Path) -> "OrderedDict[str, np.ndarray]":
     if p.suffix in (".pt", ".pth", ".bin"):
         import torch
         return normalize_keys(torch.load(str(p), map_location="cpu", weights_only=True))
-    raise ValueError(f"unsupported weight file {p} (use .safetensors, .npz or .pt)")
+    raise ValueError(f"unsupported weight file {p} (use .safetensors, .npz, .pt or .onnx)")

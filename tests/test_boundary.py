@@ -71,6 +71,7 @@ def test_class_constants_match_reference():
         (np.zeros((1, 2400, 1), np.int32), [0.0], TypeError),                   # bad state type
         (np.zeros((1, 2400, 1), np.int32), np.zeros((2, 219729), np.float16), ValueError),
         (np.zeros((1, 2400, 1), np.int32), np.zeros((1, 219729), np.float32), ValueError),
+        (np.zeros((0, 2400, 1), np.int32), None, ValueError),                   # B = 0: min() of empty
     ],
 )
 def test_input_validation_matches_onnx_wrapper(chunk, state, exc):

@@ -204,3 +204,125 @@ def test_forward_offline_matches_oracle_decode(session, make_audio):
         out, st = O.pipeline_step(logp.cpu().numpy()[0], st, i == len(padded) - 1)
         want += out
     assert [(p.text, p.start_time, p.end_time) for p in got] == want
+
+
+# --------------------------------------------------------------------------- scheduler (CPU)
+class _FakePipe:
+    """Stands in for StreamingGreedyPipeline: records every batch the scheduler forms."""
+
+    def __init__(self, max_batch):
+        self.session = type("S", (), {"max_batch": max_batch})()
+        self.batches, self.open, self._next = [], set(), 0
+
+    def open_stream(self):
+        self._next += 1
+        self.open.add(self._next)
+        return self._next
+
+    def close_stream(self, slot):
+        self.open.remove(slot)
+
+    def forward(self, chunks, slots, is_last):
+        assert len(slots) == len(set(slots)) <= self.session.max_batch
+        self.batches.append((list(slots), [int(c[0]) for c in chunks], list(is_last)))
+        return [[P.TextPhrase(f"{s}:{int(c[0])}", 0.0, 0.0)] for s, c in zip(slots, chunks)]
+
+
+def test_scheduler_packs_oldest_first_one_chunk_per_stream():
+    pipe = _FakePipe(max_batch=2)
+    sch = P.StreamScheduler(pipe)
+    ch = lambda v: np.full(2400, v, np.int32)   # noqa: E731
+    sch.submit("a", ch(1))
+    sch.submit("a", ch(2))
+    sch.submit("b", ch(10))
+    sch.submit("c", ch(20), is_last=True)
+    sch.submit("a", ch(3), is_last=True)
+    with pytest.raises(ValueError):
+        sch.submit("c", ch(21))                   # after its last chunk
+    out1 = sch.step()                             # oldest waiting: a(1), b(10)
+    assert sorted(out1) == ["a", "b"] and pipe.batches[-1][1] == [1, 10]
+    out2 = sch.step()                             # a(2) (seq 1) before c(20) (seq 3)
+    assert pipe.batches[-1][1] == [2, 20] and pipe.batches[-1][2] == [False, True]
+    assert "c" in out2 and sch.active_streams == 2   # c closed after its last chunk
+    out3 = sch.step()
+    assert pipe.batches[-1][1] == [3] and list(out3) == ["a"]
+    assert sch.step() == {} and sch.pending == 0 and sch.active_streams == 1   # b stays open, idle
+    with pytest.raises(ValueError):
+        sch.submit("b", np.zeros(2399, np.int32))
+
+
+# --------------------------------------------------------------------------- slots vs oracle (GPU)
+@pytest.fixture(scope="module")
+def oracle():
+    from tone_oracle import ToneOracle
+    from tone_amd.weights import synthetic_weights
+    return ToneOracle(synthetic_weights(0))
+
+
+@pytest.mark.gpu
+def test_ping_pong_rows_vs_oracle(session, oracle):
+    """Streams that join late and sit idle for several steps (their rows untouched, no state copy):
+    every stepping stream's logprobs vs the oracle stepped from that stream's device state, <= 1e-3;
+    idle streams' states bit-identical across the steps they skip."""
+    import torch
+    rng = np.random.default_rng(19)
+    pipe = P.StreamingGreedyPipeline(session, n_slots=6)
+    try:
+        sched = [["A"], ["A", "B"], ["B", "C", "D"], ["A", "D"], ["A", "B", "C", "D"], ["C"], ["A", "B", "C", "D"]]
+        slot = {}
+        for names in sched:
+            for k in names:
+                if k not in slot:
+                    slot[k] = pipe.open_stream()
+            idle = {k: pipe.state_of(s).clone() for k, s in slot.items() if k not in names}
+            before = np.stack([pipe.state_of(slot[k]).cpu().numpy() for k in names])
+            chunks = _pcm(rng, len(names))
+            pipe.forward(chunks, [slot[k] for k in names])
+            lp = pipe._logp[:len(names)].cpu().numpy()
+            lp_o, st_o = oracle.step(chunks, before)
+            assert np.abs(lp - lp_o).max() < 1e-3, np.abs(lp - lp_o).max()
+            after = np.stack([pipe.state_of(slot[k]).cpu().numpy() for k in names]).astype(np.float32)
+            assert np.mean(np.abs(after - st_o.astype(np.float32)) <= 2 * np.abs(np.spacing(st_o)).astype(np.float32)) > 0.995
+            for k, t in idle.items():
+                assert torch.equal(pipe.state_of(slot[k]), t), f"idle stream {k} state changed"
+    finally:
+        session.set_frame_info(None)
+
+
+@pytest.mark.gpu
+def test_scheduler_matches_single_stream_decode(session):
+    """Uneven arrivals through StreamScheduler (max_batch 3 < 5 streams, streams start and end at
+    different steps) give each stream the same phrases as decoding it alone."""
+    rng = np.random.default_rng(23)
+    audio = {}
+    for k in range(5):
+        a = np.clip(rng.normal(0, 2500, 2400 * int(rng.integers(3, 9))), -32768, 32767).astype(np.int32)
+        a[2400:2400 * 2] = 0
+        audio[k] = a.reshape(-1, 2400)
+    pipe = P.StreamingGreedyPipeline(session, n_slots=8)
+    sch = P.StreamScheduler(pipe, max_batch=3)
+    try:
+        pos = {k: 0 for k in audio}
+        got = {k: [] for k in audio}
+        t = 0
+        while any(pos[k] < len(audio[k]) for k in audio):
+            for k in audio:       # stream k delivers a chunk every (k % 2 + 1) ticks, starting at tick k
+                if t >= k and (t - k) % (k % 2 + 1) == 0 and pos[k] < len(audio[k]):
+                    sch.submit(k, audio[k][pos[k]], is_last=pos[k] == len(audio[k]) - 1)
+                    pos[k] += 1
+            for k, ph in sch.step().items():
+                got[k] += ph
+            t += 1
+        for k, ph in sch.drain().items():
+            got[k] += ph
+        assert sch.active_streams == 0
+        for k in audio:
+            want = []
+            s = pipe.open_stream()
+            for i, ch in enumerate(audio[k]):
+                want += pipe.forward(ch[None], [s], [i == len(audio[k]) - 1])[0]
+            pipe.close_stream(s)
+            assert [(p.text, p.start_time, p.end_time) for p in got[k]] == \
+                   [(p.text, p.start_time, p.end_time) for p in want]
+    finally:
+        session.set_frame_info(None)

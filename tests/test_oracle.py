@@ -35,7 +35,13 @@ def test_mel_matches_reference_features(oracle):
 
 def test_stream_matches_reference_step(oracle):
     """Tone.forward_for_export composed from the reference modules: 4 streams x 6 chunks with
-    staggered restarts (mhsa_len 0..30 mixed in one batch)."""
+    staggered restarts (mhsa_len 0..30 mixed in one batch).
+
+    Bound 5e-4 (measured 3.7e-4 at chunk 3).  It is not arithmetic error -- one step from a shared
+    state agrees to 1.3e-5 (test_oracle_step_matches_forward_for_export) -- but fp16 rounding-boundary
+    flips: a feature or state value whose fp32 pre-image differs in the last bits can round to the
+    neighbouring fp16 value (~0.2 % of state elements per step), and each flip moves later logprobs by
+    ~1e-4.  Chunk 0 (zero state, only the feature rounding) is already 1.3e-4."""
     g = np.load(GOLDEN / "golden_stream.npz")
     pcm = g["pcm"].astype(np.int32)
     B, N = pcm.shape[:2]
@@ -45,7 +51,7 @@ def test_stream_matches_reference_step(oracle):
         state[np.arange(B) > c] = 0
         logp, state = oracle.step(pcm[:, c], state)
         ref = g["logprobs"][:, c]
-        assert np.abs(logp - ref).max() < 1e-3
+        assert np.abs(logp - ref).max() < 5e-4
         np.testing.assert_array_equal(logp.argmax(-1), ref.argmax(-1))
         ds = np.abs(state[:, idx].astype(np.float32) - g["state_samples"][:, c].astype(np.float32))
         assert ds.max() <= 4e-3
@@ -109,3 +115,65 @@ def test_synthetic_weights_cover_reference_catalogue():
     # deterministic and seed dependent
     np.testing.assert_array_equal(w["decoder.decoder_layers.0.weight"], synthetic_weights(0)["decoder.decoder_layers.0.weight"])
     assert not np.array_equal(w["decoder.decoder_layers.0.weight"], synthetic_weights(1)["decoder.decoder_layers.0.weight"])
+
+
+# ---- pinned to Tone.forward_for_export itself (tests/golden/make_golden_fx.py) --------------------
+FX = GOLDEN / "golden_fx.npz"
+
+
+def test_oracle_step_matches_forward_for_export():
+    """One step from a carried state through the reference's own forward_for_export (fp32, no
+    feature rounding): every encoder stage within 2e-5 abs (measured 6.7e-6 on values up to 5.7),
+    logprobs within 5e-5 (measured 1.3e-5), next state within one fp16 ulp (or 8e-6) with >= 99.5 % of the
+    sampled elements bit-identical (measured 99.8 %)."""
+    g = np.load(FX)
+    orc = ToneOracle(synthetic_weights(0), round_feats=False)
+    trace = []
+    lp, st = orc.step(g["step_pcm"].astype(np.int32), g["step_state_in"], trace=trace)
+    for i, t in enumerate(trace[1:]):
+        ref = g["step_stages_fp32"][:, i, : t.shape[1]]
+        assert np.abs(t - ref).max() < 2e-5, f"stage {i}: {np.abs(t - ref).max():.3g}"
+    assert np.abs(lp - g["step_logprobs_fp32"]).max() < 5e-5
+    ss = int(g["state_sample"])
+    got, ref = st[:, ::ss].astype(np.float32), g["step_state_out_fp32"].astype(np.float32)
+    d = np.abs(got - ref)
+    # one fp16 ulp, or 8e-6 absolute for small values whose fp32 pre-image carries cancellation error
+    assert np.all(d <= np.maximum(np.abs(np.spacing(g["step_state_out_fp32"])).astype(np.float32), 8e-6))
+    assert np.mean(d == 0) >= 0.995
+
+
+def test_oracle_stream_matches_forward_for_export():
+    """The 6-chunk staggered streams through forward_for_export (fp32): <= 3e-4 (measured 1.6e-4,
+    fp16 state-rounding flips accumulating as above), argmax identical."""
+    g, gs = np.load(FX), np.load(GOLDEN / "golden_stream.npz")
+    pcm = gs["pcm"].astype(np.int32)
+    B, N = pcm.shape[:2]
+    orc = ToneOracle(synthetic_weights(0), round_feats=False)
+    st = np.zeros((B, C.STATE_SIZE), np.float16)
+    for c in range(N):
+        st[np.arange(B) > c] = 0
+        lp, st = orc.step(pcm[:, c], st)
+        ref = g["stream_fp32_logprobs"][:, c]
+        assert np.abs(lp - ref).max() < 3e-4
+        np.testing.assert_array_equal(lp.argmax(-1), ref.argmax(-1))
+
+
+def test_fp16_graph_delta_is_stated(oracle):
+    """forward_for_export under fp16 autocast with fp16 states (the ONNX export's semantics,
+    tone/scripts/export.py:411) vs the fp32 arithmetic the oracle and the HIP path implement:
+    measured 1.6e-2 max |dlogp| over the streams (1.7e-2 for one step), argmax identical.  So 1e-3
+    against an fp16 ORT graph is below that graph's own rounding noise; the bar is held against the
+    fp32 restatement instead, and this bound (2.5e-2) is the stated
+    fp16-graph delta."""
+    g, gs = np.load(FX), np.load(GOLDEN / "golden_stream.npz")
+    pcm = gs["pcm"].astype(np.int32)
+    B, N = pcm.shape[:2]
+    st = np.zeros((B, C.STATE_SIZE), np.float16)
+    worst = 0.0
+    for c in range(N):
+        st[np.arange(B) > c] = 0
+        lp, st = oracle.step(pcm[:, c], st)
+        ref = g["stream_fp16_logprobs"][:, c]
+        worst = max(worst, float(np.abs(lp - ref).max()))
+        np.testing.assert_array_equal(lp.argmax(-1), ref.argmax(-1))
+    assert 1e-3 < worst < 2.5e-2, worst
