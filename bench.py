@@ -25,7 +25,6 @@ import torch  # noqa: E402
 
 import tone_amd.config as C  # noqa: E402
 from tone_amd.model import ToneSession  # noqa: E402
-from tone_amd.shard import gather_logprobs  # noqa: E402
 from tone_amd.weights import synthetic_weights  # noqa: E402
 
 METRIC = "real-time-factor & streams/sec/node, 300 ms chunk, batch=1..4096"
@@ -94,50 +93,91 @@ def synthetic_pcm(rng, b, n_chunks, silence=0.2):
     return x.astype(np.int32)
 
 
-def cpu_baseline(budget_s: float, batch: int) -> dict:
-    """The CPU oracle (numpy port of the reference step) on a bounded sample, this host's cores."""
+def cpu_baseline(budget_s: float) -> dict:
+    """BASELINE.md 4 / SURVEY.md 8d CPU side-by-side: the step restated with batched torch CPU kernels
+    (oracle/tone_cpu.py: oneDNN/MKL GEMMs and convolutions, BatchNorm folded, fp32 with the reference's
+    fp16 rounding points) timed on this host's cores at B = 1 and B = 256, ``budget_s`` of stateful
+    steps each (after one warm-up step); median and p99 per step."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from tone_oracle import ToneOracle
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = os.cpu_count() or 1
-    orc = ToneOracle(synthetic_weights(0))
-    rng = np.random.default_rng(1)
-    pcm = synthetic_pcm(rng, batch, 4)
-    st = None
-    orc.step(pcm[0], st)  # warm-up
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        _, st = orc.step(pcm[n % 4], st)
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = (time.perf_counter() - t0) / n
-    return {"value": round(batch * C.AUDIO_CHUNK_SAMPLES / C.SAMPLE_RATE / dt, 2), "unit": "real-time streams",
-            "chunks_per_s": round(batch / dt, 2), "ms_per_step": round(dt * 1e3, 2), "cores": int(threads),
-            "kind": "port",
-            "sample": f"numpy oracle (oracle/tone_oracle.py), batch {batch}, {n} stateful steps, fp32"}
+    from tone_cpu import ToneCPU
+    cores = torch.get_num_threads()
+    cpu = ToneCPU(synthetic_weights(0))
+    out = {}
+    for b in (1, 256):
+        pcm = torch.from_numpy(synthetic_pcm(np.random.default_rng(1), b, 4))
+        st = torch.zeros((b, C.STATE_SIZE), dtype=torch.float16)
+        _, st = cpu.step(pcm[0], st)       # warm-up
+        ts = []
+        t_end = time.perf_counter() + budget_s
+        while time.perf_counter() < t_end or len(ts) < 3:
+            t0 = time.perf_counter()
+            _, st = cpu.step(pcm[len(ts) % 4], st)
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        out[f"b{b}"] = {"value": round(b * C.AUDIO_CHUNK_SAMPLES / C.SAMPLE_RATE / med, 2), "median_ms": round(med * 1e3, 2),
+                        "p99_ms": round(float(np.percentile(ts, 99)) * 1e3, 2), "steps": len(ts)}
+    return {"value": out["b256"]["value"], "unit": "real-time streams", "cores": int(cores), "kind": "port",
+            "batch": 256, "per_batch": out,
+            "sample": f"torch-CPU restatement (oracle/tone_cpu.py), fp32, stateful synthetic chunks, about {budget_s:g} s "
+                      f"of steps at each of B = 1 and B = 256 on {cores} threads; value = B = 256 median"}
 
 
-def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True):
-    """Time args.steps streaming steps of B streams per GPU; returns (elapsed_s, roofline dict | None)."""
-    sess = ToneSession(synthetic_weights(0), device=local, precision=precision, max_batch=B,
+_WEIGHTS = None
+
+
+def replica_weights(pg, dev):
+    """The checkpoint on this rank: built once on rank 0 and broadcast to the others (RCCL)."""
+    global _WEIGHTS
+    if _WEIGHTS is None:
+        if pg is None:
+            _WEIGHTS = synthetic_weights(0)
+        else:
+            from tone_amd.shard import broadcast_weights
+            _WEIGHTS = broadcast_weights(synthetic_weights(0) if pg.get_rank() == 0 else None,
+                                         device=dev if pg.get_backend() == "nccl" else None)
+    return _WEIGHTS
+
+
+def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True, cap=None):
+    """Time args.steps streaming steps of B streams on this GPU; returns a dict with the max-over-ranks
+    elapsed time, per-step percentiles (HIP events on the launch stream) and the roofline (rank 0).
+
+    With pg (N > 1) each step's logprobs are all-gathered to every rank (the host-decoding exchange,
+    SURVEY.md 8e) on a separate stream, overlapped with the next step: logprobs are double-buffered and
+    step i + 2 waits only for the gather that read its buffer.  ``cap`` (largest shard) pads unequal
+    shards so the collective has equal parts."""
+    cap = cap or B
+    sess = ToneSession(replica_weights(pg, dev), device=local, precision=precision, max_batch=B,
                        graph=not args.no_graph)
     rng = np.random.default_rng(1000 + rank)
     pcm = torch.from_numpy(synthetic_pcm(rng, B, args.chunks)).to(dev)             # (chunks, B, 2400)
     slabs = [torch.zeros((B, C.STATE_SIZE), dtype=torch.float16, device=dev) for _ in range(2)]
     signal = torch.empty((B, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32, device=dev)   # audio lands here
-    logp = torch.empty((B, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev)
+    logp = [torch.zeros((cap, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev) for _ in range(2)]
+    gathered = [torch.empty((world * cap, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev)
+                for _ in range(2)] if pg is not None else None
     stream = torch.cuda.Stream(dev)
+    comm = torch.cuda.Stream(dev) if pg is not None else None
+    freed = [None, None]          # event: the gather that last read logp[k] is done
 
     def step(i: int) -> None:
+        k = i % 2
+        if freed[k] is not None:
+            stream.wait_event(freed[k])
         signal.copy_(pcm[i % args.chunks], non_blocking=True)
-        sess.run(signal, slabs[i % 2], logp, slabs[(i + 1) % 2], stream=stream)
-        if pg is not None:   # host-decoding exchange: every rank's logprobs, in stream order
-            gather_logprobs(logp, world * B)
+        sess.run(signal, slabs[k], logp[k][:B], slabs[1 - k], stream=stream)
+        if pg is not None:
+            ready = stream.record_event()
+            with torch.cuda.stream(comm):
+                comm.wait_event(ready)
+                if args.dist_backend == "gloo":      # one-GPU rehearsal: gloo gathers host tensors
+                    comm.synchronize()
+                    host = torch.empty((world * cap, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32)
+                    pg.all_gather_into_tensor(host, logp[k].cpu())
+                    gathered[k].copy_(host)
+                else:
+                    pg.all_gather_into_tensor(gathered[k], logp[k])
+                freed[k] = comm.record_event()
 
     torch.cuda.synchronize()
     with torch.cuda.stream(stream):
@@ -147,29 +187,35 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True)
     if pg is not None:
         pg.barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
         for i in range(args.warmup, args.warmup + args.steps):
+            ev[i - args.warmup].record(stream)
             step(i)
+        ev[-1].record(stream)
     torch.cuda.synchronize()
     if pg is not None:
         pg.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if pg is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
         elapsed = float(t.item())
+    per_step = np.array([ev[j].elapsed_time(ev[j + 1]) for j in range(args.steps)])
+    res = {"elapsed": elapsed, "median_ms": round(float(np.median(per_step)), 4),
+           "p99_ms": round(float(np.percentile(per_step, 99)), 4)}
 
     # ---- roofline of the dominant kernel: per-kernel HIP events on the launch stream -----------
-    roof = None
+    res["roofline"] = None
     if rank == 0 and with_roofline:
         sess.set_graph(False)
         sess.set_timing(True)
         with torch.cuda.stream(stream):
             for i in range(args.steps):
                 signal.copy_(pcm[i % args.chunks], non_blocking=True)
-                sess.run(signal, slabs[i % 2], logp, slabs[(i + 1) % 2], stream=stream)
+                sess.run(signal, slabs[i % 2], logp[0][:B], slabs[(i + 1) % 2], stream=stream)
         torch.cuda.synchronize()
         per_stream = family_flops_per_stream()
         fams = {}
@@ -184,35 +230,56 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True)
         achieved = f["flop_per_launch"] / (f["avg_us"] * 1e-6) / 1e12
         peak = PEAK_TFLOPS[precision]
         traffic, tsrc = measured_traffic(dom, precision, B)
+        gemm_us = sum(v["avg_us"] * v["launches_per_step"] for v in fams.values())
+        gemm_flop = sum(per_stream.values()) * B
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": tsrc, "algo_bytes": int(algo_bytes(dom, precision, B)),
                 "avg_us": round(f["avg_us"], 2), "flop_per_launch": int(f["flop_per_launch"]),
                 "step_tflops": round(C.FLOP_PER_CHUNK * B / (elapsed / args.steps) / 1e12, 2),
+                "encoder_gemm_tflops": round(gemm_flop / (gemm_us * 1e-6) / 1e12, 2),
+                "encoder_gemm_frac": round(gemm_flop / (gemm_us * 1e-6) / 1e12 / peak, 4),
+                "step_io_gbs": round(B * C.IO_BYTES_PER_CHUNK / (elapsed / args.steps) / 1e9, 1),
                 "families_us_per_step": {k: round(v["avg_us"] * v["launches_per_step"], 1) for k, v in fams.items()}}
         if precision == "fp32":
             roof["gemm_arith"] = ("fp32 as exact 3-way bf16 splits, 6 products per multiply-add on "
                                   "v_mfma_f32_32x32x16_bf16 (fp32-accurate; tests/test_gpu_parity.py)")
             roof["pipe_peak"] = round(SPLIT_PIPE_PEAK, 1)
             roof["pipe_frac"] = round(achieved / SPLIT_PIPE_PEAK, 4)
+        res["roofline"] = roof
     sess.close()
-    del slabs, pcm
+    del slabs, pcm, logp, gathered
     torch.cuda.empty_cache()
-    return elapsed, roof
+    return res
+
+
+def workload_line(name, res, n_streams, steps, dtype, **extra):
+    dt = res["elapsed"] / steps
+    return {"workload": name, "value": round(n_streams / dt * C.AUDIO_CHUNK_SAMPLES / C.SAMPLE_RATE, 1),
+            "unit": "real-time streams", "ms_per_step": round(dt * 1e3, 4), "median_ms": res["median_ms"],
+            "p99_ms": res["p99_ms"], "chunks_per_s": round(n_streams / dt, 1), "rtf": round(dt * 1e3 / 300.0, 5),
+            "dtype": dtype, **extra, "roofline": res["roofline"]}
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=300, help="timed steps (300 x 3.6 ms: a window of about 1 s)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="streams per GPU (BASELINE config 2: 256)")
+    ap.add_argument("--batch", type=int, default=256, help="streams per GPU, weak scaling (BASELINE config 2: 256)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="total streams split over the GPUs, strong scaling (BASELINE config 4: 4096); "
+                         "replaces --batch for the headline")
     ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "bf16"], default="fp32")
     ap.add_argument("--chunks", type=int, default=10, help="distinct 300 ms chunks cycled per stream")
-    ap.add_argument("--cpu-baseline-s", type=float, default=12.0, help="CPU oracle budget (0 = skip)")
-    ap.add_argument("--cpu-baseline-batch", type=int, default=32)
+    ap.add_argument("--cpu-baseline-s", type=float, default=8.0, help="CPU baseline budget per batch (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: rehearse N > 1 on one GPU (ranks share the card, collectives staged through host)")
     ap.add_argument("--alt", type=int, default=1, help="also measure BASELINE config 3 (bf16, B=2048) at N=1")
+    ap.add_argument("--config4", type=int, default=4096,
+                    help="also measure BASELINE config 4: this many streams in total, sharded over the N GPUs, "
+                         "bf16, logprobs all-gathered (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,35 +287,57 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)")
+    if args.dist_backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         pg = dist
 
-    B = args.batch
-    elapsed, roof = measure(args, B, args.precision, dev, local, world, rank, pg)
-    ms_step = elapsed / args.steps * 1e3
-    chunks_s = world * B / (elapsed / args.steps)
+    from tone_amd.shard import shard_sizes
+    if args.global_batch:
+        sizes = shard_sizes(args.global_batch, world)
+        B, cap, total, scaling = sizes[rank], max(sizes), args.global_batch, "strong"
+    else:
+        B, cap, total, scaling = args.batch, args.batch, world * args.batch, "weak"
+    res = measure(args, B, args.precision, dev, local, world, rank, pg, cap=cap)
+    ms_step = res["elapsed"] / args.steps * 1e3
+    chunks_s = total / (res["elapsed"] / args.steps)
     streams = chunks_s * C.AUDIO_CHUNK_SAMPLES / C.SAMPLE_RATE
 
+    alts = []
     # BASELINE config 3 (1 GPU, batch 2048, bf16 MFMA, stateful) reported beside the headline
-    alt = None
     if world == 1 and args.alt:
-        e2, r2 = measure(args, 2048, "bf16", dev, local, world, rank, pg)
-        cs2 = 2048 / (e2 / args.steps)
-        alt = {"workload": "BASELINE config 3: streaming step, batch 2048, bf16 MFMA GEMMs, stateful 300 ms chunks",
-               "value": round(cs2 * C.AUDIO_CHUNK_SAMPLES / C.SAMPLE_RATE, 1), "unit": "real-time streams",
-               "ms_per_step": round(e2 / args.steps * 1e3, 4), "chunks_per_s": round(cs2, 1),
-               "rtf": round(e2 / args.steps * 1e3 / 300.0, 5), "dtype": "bf16", "roofline": r2}
+        r2 = measure(args, 2048, "bf16", dev, local, world, rank, pg)
+        alts.append(workload_line("BASELINE config 3: streaming step, batch 2048, bf16 MFMA GEMMs, stateful 300 ms "
+                                  "chunks", r2, 2048, args.steps, "bf16", n_gpus=1, scaling="n/a"))
+    # BASELINE config 4 (4096 streams over the node's GPUs, strong scaling, RCCL all-gather of logprobs)
+    if args.config4 and not (args.global_batch == args.config4 and args.precision == "bf16"):
+        sizes = shard_sizes(args.config4, world)
+        r4 = measure(args, sizes[rank], "bf16", dev, local, world, rank, pg, cap=max(sizes))
+        alts.append(workload_line(
+            f"BASELINE config 4: {args.config4} streams sharded {max(sizes)}/GPU over {world} GPU(s), bf16 MFMA "
+            f"GEMMs, RCCL all-gather of logprobs per step (overlapped), strong scaling", r4, args.config4,
+            args.steps, "bf16", n_gpus=world, global_batch=args.config4, batch_per_gpu=max(sizes), scaling="strong"))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_s > 0:
-        cpu = cpu_baseline(args.cpu_baseline_s, args.cpu_baseline_batch)
+        cpu = cpu_baseline(args.cpu_baseline_s)
 
     if rank == 0:
+        if args.global_batch:
+            wl = (f"streaming step, {total} streams sharded {cap}/GPU over {world} GPU(s), {args.precision}, "
+                  f"stateful 300 ms chunks, strong scaling")
+        elif args.precision == "fp32" and B == 256:
+            wl = "BASELINE config 2: streaming step, batch 256/GPU, fp32, stateful 300 ms chunks"
+        else:
+            wl = f"streaming step, batch {B}/GPU, {args.precision}, stateful 300 ms chunks"
         out = {
             "metric": METRIC,
             "value": round(streams, 1),
@@ -257,22 +346,23 @@ def main() -> None:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
+            "median_ms": res["median_ms"],
+            "p99_ms": res["p99_ms"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (Gaussian sigma=3000 int16 PCM, 20% silent chunks; random-init T-one weights)",
-            "config": {"workload": "BASELINE config 2: streaming step, batch 256/GPU, fp32, stateful 300 ms chunks"
-                       if args.precision == "fp32" and B == 256 else
-                       f"streaming step, batch {B}/GPU, {args.precision}, stateful 300 ms chunks",
-                       "model": "T-one 71.7M (16-layer chunked Conformer, d384)",
-                       "batch_per_gpu": B, "global_batch": world * B, "chunk_ms": 300,
-                       "parallelism": f"dp{world}", "graph": not args.no_graph},
+            "config": {"workload": wl, "model": "T-one 71.7M (16-layer chunked Conformer, d384)",
+                       "batch_per_gpu": cap, "global_batch": total, "chunk_ms": 300,
+                       "parallelism": f"dp{world}", "graph": not args.no_graph,
+                       "collective": "RCCL all_gather_into_tensor of logprobs per step, overlapped" if world > 1
+                       else None},
             "chunks_per_s": round(chunks_s, 1),
             "rtf": round(ms_step / 300.0, 5),
-            "roofline": roof,
+            "roofline": res["roofline"],
             "cpu_baseline": cpu,
-            "alt_workloads": [alt] if alt else [],
+            "alt_workloads": alts,
         }
         print(json.dumps(out), flush=True)
     if pg is not None:

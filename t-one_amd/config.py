@@ -116,3 +116,5 @@ FLOP_PER_CHUNK_ENCODER_HEAD = 1_285_872_640
 FLOP_PER_CHUNK_MEL = 1_870_000
 FLOP_PER_CHUNK = FLOP_PER_CHUNK_ENCODER_HEAD + FLOP_PER_CHUNK_MEL
 STATE_BYTES = 2 * STATE_SIZE
+# algorithmic HBM bytes one stream-chunk moves at the boundary: state in + out, PCM in, logprobs out
+IO_BYTES_PER_CHUNK = 2 * STATE_BYTES + 4 * 2400 + 4 * 10 * 35

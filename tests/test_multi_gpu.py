@@ -1,0 +1,55 @@
+"""World-2 runs on the one GPU of the box: real ToneSessions per rank (tests/world2_worker.py) and
+bench.py's N > 1 path (weight broadcast, strong-scaling shards, double-buffered all-gather) rehearsed
+with the gloo backend, since RCCL needs one card per rank.  Both are started as child processes of
+torchrun (never exec'd from this process)."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(args, timeout):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.gpu
+def test_world2_sessions_gather_matches_single_process(tmp_path):
+    out = tmp_path / "w2.json"
+    r = _torchrun([os.path.join(ROOT, "tests", "world2_worker.py"), str(out)], timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["world"] == 2 and res["shape"] == [7, 10, 35]
+    # the gathered shards equal the one-process batch (streams are independent; same kernels)
+    assert res["d_single"] <= 1e-5, res
+    assert res["d_oracle"] < 1e-3, res
+
+
+@pytest.mark.gpu
+def test_bench_world2_strong_scaling_rehearsal():
+    r = _torchrun(["bench.py", "--gpus", "2", "--dist-backend", "gloo", "--global-batch", "64", "--steps", "4",
+                   "--warmup", "1", "--alt", "0", "--config4", "32", "--cpu-baseline-s", "0"], timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["config"]["global_batch"] == 64
+    assert out["config"]["batch_per_gpu"] == 32 and out["value"] > 0
+    c4 = out["alt_workloads"][0]
+    assert c4["global_batch"] == 32 and c4["batch_per_gpu"] == 16 and c4["scaling"] == "strong"

@@ -85,3 +85,33 @@ def test_gloo_world2_gather_matches_single_process(n_streams):
     for rank, err, shape in res:
         assert shape == (n_streams, 10, 35)
         assert err < 1e-4, (rank, err)
+
+
+def _bcast_worker(rank, world, port, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tone_amd.shard import broadcast_weights
+        from tone_amd.weights import synthetic_weights
+        w = broadcast_weights(synthetic_weights(0) if rank == 0 else None)
+        ref = synthetic_weights(0)
+        ok = list(w) == list(ref) and all(np.array_equal(w[k], ref[k]) for k in ref)
+        result_q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_weight_broadcast():
+    """One checkpoint load on rank 0, broadcast once: every rank holds the identical replica."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res), res
