@@ -266,25 +266,38 @@ def test_fp32_split_vs_fp32_mfma(weights, oracle):
     assert errs["fp32"] <= 2 * errs["fp32-mfma"] + 1e-5, errs
 
 
+# bf16 bounds, measured (scripts/bf16_measure.py, profiles/r02_bf16_bounds.json): B = 2048, 10 stateful
+# chunks, staggered starts, 64 sampled streams -- max |dlogp| 0.043-0.051 per chunk, p99 0.030-0.032,
+# argmax 100 % identical.  Bounds: max 0.08, p99 0.05, argmax identical wherever the oracle's top-2 margin
+# exceeds 0.1 and >= 99.5 % overall.
+BF16_MAX, BF16_P99, BF16_MARGIN = 0.08, 0.05, 0.1
+
+
+def assert_bf16_close(lp, ref, what=""):
+    d = np.abs(lp - ref)
+    assert d.max() < BF16_MAX and np.percentile(d, 99) < BF16_P99, \
+        f"{what} max {d.max():.3g} p99 {np.percentile(d, 99):.3g}"
+    srt = np.sort(ref, axis=-1)
+    clear = (srt[..., -1] - srt[..., -2]) > BF16_MARGIN
+    np.testing.assert_array_equal(lp.argmax(-1)[clear], ref.argmax(-1)[clear], err_msg=f"{what} argmax")
+    assert np.mean(lp.argmax(-1) == ref.argmax(-1)) >= 0.995, what
+
+
 def test_bf16_mode_close_to_oracle(weights, oracle):
-    """BASELINE config 3 arithmetic: bf16 MFMA operands, fp32 accumulate/norms/softmax."""
+    """BASELINE config 3 arithmetic: bf16 MFMA operands, fp32 accumulate/norms/softmax (small batch)."""
     _gpu()
     from tone_amd.model import ToneSession
     s = ToneSession(weights, precision="bf16", max_batch=64)
     rng = np.random.default_rng(13)
     b = 32
     st = np.zeros((b, C.STATE_SIZE), np.float16)
-    agree, worst = [], 0.0
+    st_o = st.copy()
     for c in range(3):
         pcm = synthetic_pcm(rng, b)
-        lp_g, st_g = gpu_step(s, pcm, st)
-        lp_o, _ = oracle.step(pcm, st)
-        worst = max(worst, float(np.abs(lp_g - lp_o).max()))
-        agree.append(np.mean(lp_g.argmax(-1) == lp_o.argmax(-1)))
-        st = st_g
+        lp_g, st = gpu_step(s, pcm, st)
+        lp_o, st_o = oracle.step(pcm, st_o)
+        assert_bf16_close(lp_g, lp_o, f"chunk {c}")
     s.close()
-    assert worst < 0.25, worst
-    assert np.mean(agree) > 0.97, agree
 
 
 def test_bf16_pre_encode_stage(weights, oracle):
@@ -311,26 +324,56 @@ def test_bf16_pre_encode_stage(weights, oracle):
     assert rel < 2e-2, rel
 
 
-def test_bf16_large_batch_paths(weights, oracle):
-    """bf16 at a batch large enough for the persistent / two-workgroup GEMM paths (M = 20480 rows):
-    a sample of the streams against the oracle, same bounds as the small-batch bf16 check."""
+def test_bf16_config3_staggered_streams(weights, oracle):
+    """BASELINE config 3 as specified: B = 2048 bf16, 10 stateful 300 ms chunks, stream s
+    starting (zero state) at chunk s % 4; 64 sampled streams stepped independently by the oracle (its own
+    fp32 state chain, not the device state) and compared every chunk."""
     _gpu()
     from tone_amd.model import ToneSession
-    b, pick = 2048, np.arange(0, 2048, 64)
+    b, n = 2048, 10
+    pick = np.arange(0, b, 32)
     s = ToneSession(weights, precision="bf16", max_batch=b)
     rng = np.random.default_rng(17)
-    st = np.zeros((b, C.STATE_SIZE), np.float16)
+    off = np.arange(b) % 4
+    st = torch.zeros((b, C.STATE_SIZE), dtype=torch.float16, device=s.dev)
     st_o = np.zeros((len(pick), C.STATE_SIZE), np.float16)
-    agree, worst = [], 0.0
-    for c in range(2):
-        pcm = synthetic_pcm(rng, b)
-        lp_g, st = gpu_step(s, pcm, st)
-        lp_o, st_o = oracle.step(pcm[pick], st_o)
-        worst = max(worst, float(np.abs(lp_g[pick] - lp_o).max()))
-        agree.append(np.mean(lp_g[pick].argmax(-1) == lp_o.argmax(-1)))
-    s.close()
-    assert worst < 0.25, worst
-    assert np.mean(agree) > 0.97, agree
+    try:
+        for c in range(n):
+            pcm = synthetic_pcm(rng, b)
+            st[torch.from_numpy(off == c).to(s.dev)] = 0
+            st_o[off[pick] == c] = 0
+            lp, st = s.step(torch.from_numpy(pcm).to(s.dev), st)
+            lp_o, st_o = oracle.step(pcm[pick], st_o)
+            live = off[pick] <= c
+            assert_bf16_close(lp.cpu().numpy()[pick][live], lp_o[live], f"chunk {c}")
+    finally:
+        s.close()
+
+
+def test_bf16_example_audio_greedy_decode(weights, oracle):
+    """Greedy decode of the reference's example utterance in bf16 mode == the oracle decode of the fp32
+    oracle's logprobs (phrases, times and every frame's greedy token)."""
+    _gpu()
+    import tone_decode_oracle as O
+    from tone_amd.model import ToneSession
+    audio = np.load(GOLDEN / "audio_short_pcm.npy").astype(np.int32)
+    padded = np.pad(audio, (O.PADDING, O.PADDING))
+    padded = np.pad(padded, (0, -len(padded) % 2400)).reshape(-1, 2400)
+    s = ToneSession(weights, precision="bf16", max_batch=1)
+    try:
+        state, so, sg, sw, got, want = None, None, None, None, [], []
+        for i, ch in enumerate(padded):
+            lp, state = s.step(torch.from_numpy(ch[None]).to(s.dev), state)
+            lp = lp.cpu().numpy()[0]
+            lpo, so = oracle.step(ch[None], so)
+            np.testing.assert_array_equal(lp.argmax(-1), lpo[0].argmax(-1))
+            out, sg = O.pipeline_step(lp, sg, i == len(padded) - 1)
+            got += out
+            out, sw = O.pipeline_step(lpo[0], sw, i == len(padded) - 1)
+            want += out
+    finally:
+        s.close()
+    assert got == want and len(want) > 0
 
 
 @pytest.mark.gpu
