@@ -31,6 +31,8 @@
 // partials go to a workspace and a second kernel sums them in a fixed order (deterministic) and
 // applies the epilogue.
 #include "common.h"
+
+#include <cstdlib>
 #include "kernels.h"
 
 #include <type_traits>
@@ -934,6 +936,16 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   constexpr int kTarget = 512;
   // large batches: the persistent transposed-orientation kernels (gemm_t.hip, tools/gemm_bench sweep)
   const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
+  // FFN up (SwiGLU): the pipelined 16x16x32 kernel with 16-byte stores; inside the real step (scripts/ab_route.py,
+  // profiles/r02_ab_route.jsonl) it beats gemm_t by 3 % on FFN up, while pw1 (fp32 GLU output) stays on gemm_t
+  // (gemm_t.hip gemm_p_kernel; FFN up M = 20480: 72.9 vs 82.1 us, pw1 20.1 vs 22.5 us for gemm_t,
+  // scripts/gp_sweep.sh, profiles/r02_gemm_p_sweep.jsonl)
+  // TONE_GEMM_P (experiments): bit 0 SwiGLU, bit 1 GLU on gemm_p; low nibble of bits 4.. = gemm_p variant
+  const char* route_env = getenv("TONE_GEMM_P");
+  const int route = route_env ? atoi(route_env) : 1;   // in-step A/B (scripts/ab_route.py): SwiGLU only, plain stores
+  const int pv = (route >> 4) & 15;
+  if (epi == EPI_SWIGLU && (route & 1) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
+  if (epi == EPI_GLU && (route & 2) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
   if (epi == EPI_SWIGLU && a.N % 256 == 0 && t256 >= 192) return gemm_t(a, epi, 0, st);
   if (epi == EPI_GLU && a.N % 128 == 0 && (int64_t)((a.M + 127) / 128) * (a.N / 128) >= 512) return gemm_t(a, epi, 5, st);
   const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);

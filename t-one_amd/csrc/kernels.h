@@ -51,6 +51,8 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // persistent transposed-orientation bf16 GEMM (gemm_t.hip); variant = tile shape, see there
 hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
+// pipelined 256x256 bf16 GEMM on v_mfma_f32_16x16x32_bf16 (gemm_t.hip gemm_p_kernel); variant: 0, 1 = + static priority
+hipError_t gemm_p(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3

@@ -194,6 +194,7 @@ int main(int argc, char** argv) {
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
       return v < 0 ? gemm(a, epi, !f32, 0)
+             : v >= 90 ? gemm_p(a, epi, v - 90, 0)
              : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
              : (v >= 50 && nsplit > 1) ? gemm_x3_splitk(a, epi, v - 50, nsplit, 0)
