@@ -28,7 +28,7 @@ from tone_amd.model import ToneSession  # noqa: E402
 from tone_amd.weights import synthetic_weights  # noqa: E402
 
 METRIC = "real-time-factor & streams/sec/node, 300 ms chunk, batch=1..4096"
-PEAK_TFLOPS = {"fp32": 157.3, "fp32-mfma": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"fp32": 157.3, "fp32-mfma": 157.3, "bf16": 2500.0, "fp8": 5000.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
 # "fp32" runs its GEMMs as exact 3-way bf16 splits: 6 bf16 MFMA products per fp32 multiply-add, so the
 # matrix pipe's own ceiling for that arithmetic is the bf16 dense peak / 6
 SPLIT_PIPE_PEAK = 2500.0 / 6
@@ -270,7 +270,7 @@ def main() -> None:
     ap.add_argument("--global-batch", type=int, default=0,
                     help="total streams split over the GPUs, strong scaling (BASELINE config 4: 4096); "
                          "replaces --batch for the headline")
-    ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "bf16"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "bf16", "fp8"], default="fp32")
     ap.add_argument("--chunks", type=int, default=10, help="distinct 300 ms chunks cycled per stream")
     ap.add_argument("--cpu-baseline-s", type=float, default=8.0, help="CPU baseline budget per batch (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
@@ -280,6 +280,9 @@ def main() -> None:
     ap.add_argument("--config4", type=int, default=4096,
                     help="also measure BASELINE config 4: this many streams in total, sharded over the N GPUs, "
                          "bf16, logprobs all-gathered (0 = skip)")
+    ap.add_argument("--config5", type=int, default=4096,
+                    help="also measure BASELINE config 5's device step: this many streams sharded over the N GPUs, "
+                         "MXFP8 q/k/v + FFN GEMMs, logprobs all-gathered (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -325,6 +328,18 @@ def main() -> None:
             f"BASELINE config 4: {args.config4} streams sharded {max(sizes)}/GPU over {world} GPU(s), bf16 MFMA "
             f"GEMMs, RCCL all-gather of logprobs per step (overlapped), strong scaling", r4, args.config4,
             args.steps, "bf16", n_gpus=world, global_batch=args.config4, batch_per_gpu=max(sizes), scaling="strong"))
+
+    # BASELINE config 5 (4096 streams, fp8 MFMA on the q/k/v and FFN weights); the host KenLM beam search
+    # consumes the gathered logprobs outside the device step (pipeline.StreamingGreedyPipeline(decoder=...))
+    if args.config5:
+        sizes = shard_sizes(args.config5, world)
+        r5 = measure(args, sizes[rank], "fp8", dev, local, world, rank, pg, cap=max(sizes))
+        alts.append(workload_line(
+            f"BASELINE config 5 (device step): {args.config5} streams sharded {max(sizes)}/GPU over {world} GPU(s), "
+            f"MXFP8 (e4m3 + E8M0 per 32) q/k/v and FFN GEMMs on v_mfma_scale_f32_16x16x128_f8f6f4, bf16 elsewhere, "
+            f"RCCL all-gather of logprobs per step; the host KenLM beam decode of the gathered logprobs is not in "
+            f"the timed step (pyctcdecode/kenlm are not installed)", r5, args.config5, args.steps, "fp8", n_gpus=world,
+            global_batch=args.config5, batch_per_gpu=max(sizes), scaling="strong"))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_s > 0:

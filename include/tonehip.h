@@ -44,6 +44,9 @@ extern "C" {
                                    /* on v_mfma_f32_32x32x16_bf16: fp32-accurate, BASELINE config 2      */
 #define TONE_PRECISION_BF16 1      /* bf16 MFMA operands, fp32 accumulate, BASELINE config 3            */
 #define TONE_PRECISION_FP32_MFMA 2 /* fp32 GEMMs on the exact-fp32 MFMA (v_mfma_f32_32x32x2_f32)       */
+#define TONE_PRECISION_FP8 3       /* bf16 mode, with the q/k/v and FFN GEMMs on MXFP8 (e4m3 values, one */
+                                   /* E8M0 scale per 32 along K) on v_mfma_scale_f32_16x16x128_f8f6f4:   */
+                                   /* BASELINE config 5                                                   */
 
 #define TONE_OK 0
 #define TONE_E_INVALID -1   /* bad argument (shape, null pointer, unknown name)       */

@@ -1,4 +1,4 @@
-"""Measure the bf16 mode (BASELINE config 3) against the fp32 oracle: B = 2048, 10 stateful chunks,
+"""Measure the bf16 (or PREC=fp8) mode (BASELINE config 3) against the fp32 oracle: B = 2048, 10 stateful chunks,
 stream s starts (zero state) at chunk s % 4; 64 sampled streams checked every chunk.  Also the
 greedy decode of the example audio in bf16 vs the oracle decode of the fp32 oracle logprobs.
 Prints JSON (used to set the bounds in tests/test_gpu_parity.py)."""
@@ -20,9 +20,10 @@ import tone_decode_oracle as O  # noqa: E402
 w = synthetic_weights(0)
 orc = ToneOracle(w)
 B, N = 2048, 10
+PREC = os.environ.get("PREC", "bf16")
 pick = np.arange(0, B, 32)
 rng = np.random.default_rng(41)
-s = ToneSession(w, precision="bf16", max_batch=B)
+s = ToneSession(w, precision=PREC, max_batch=B)
 st = torch.zeros((B, C.STATE_SIZE), dtype=torch.float16, device="cuda:0")
 st_o = np.zeros((len(pick), C.STATE_SIZE), np.float16)
 off = np.arange(B) % 4
@@ -49,7 +50,7 @@ audio = np.load(os.path.join(ROOT, "tests", "golden", "audio_short_pcm.npy")).as
 padded = np.pad(audio, (O.PADDING, O.PADDING))
 padded = np.pad(padded, (0, -len(padded) % 2400)).reshape(-1, 2400)
 res = {}
-for prec in ("bf16", "fp32"):
+for prec in (PREC, "fp32"):
     s = ToneSession(w, precision=prec, max_batch=1)
     state, sto, so, got, want, toks_g, toks_o = None, None, None, [], [], [], []
     for i, ch in enumerate(padded):

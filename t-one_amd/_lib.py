@@ -37,7 +37,7 @@ ABI_VERSION = 1
 
 # "fp32": fp32 GEMMs as exact 3-way bf16 splits on the bf16 MFMA (fp32-accurate; the default fp32 path);
 # "fp32-mfma": fp32 GEMMs on the exact-fp32 MFMA; "bf16": bf16 GEMM operands, fp32 accumulate
-PRECISION = {"fp32": 0, "bf16": 1, "fp32-mfma": 2}
+PRECISION = {"fp32": 0, "bf16": 1, "fp32-mfma": 2, "fp8": 3}
 
 _lib = None
 

@@ -1,0 +1,386 @@
+// MXFP8 projections for TONE_PRECISION_FP8 (BASELINE config 5: fp8 MFMA on the q/k/v and FFN weights).
+//
+// Format: OCP MX -- every 32 consecutive values along K share one E8M0 scale (a power of two), the
+// values are e4m3 (OCP e4m3fn, max 448).  A block with max |v| = a gets the exponent
+// E = floor(log2 a) - 8, so v / 2^E lies below 512 and e4m3's 448 clamps the top of the binade
+// (the OCP MX conversion rule).  Weights are quantized once at finalize (session.hip), activations
+// by quant_mx_kernel below or, for the FFN intermediate, directly by the up-projection's epilogue.
+//
+// GEMM: v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, E8M0 scales): twice the bf16 MFMA rate per
+// clock (MI355X_MICROARCH.md, Matrix cores).  Operand map, measured on the MI355X (tools/mx_probe.hip):
+// lane l holds row (l & 15) and the k-values 16 g .. 16 g + 15 and 64 + 16 g .. 64 + 16 g + 15 of the
+// 128-deep K-tile (g = l >> 4), and passes the scale of block g (k 32 g .. 32 g + 31) of its row.
+// Structure as gemm_p_kernel (gemm_t.hip): transposed orientation D[n][m] = W[n] . X[m], persistent
+// XCD-contiguous tiles, BNW (256 | 128) W rows x 256 X rows, K-tile = 128 fp8 = one 128-byte line per
+// row, 16 KiB quarters staged by LDS-DMA into a two-stage ring, every fragment of a K-tile read in
+// its first two MFMA phases so the stage is free after the first barrier, counted vmcnt(4) keeping
+// two quarters of K-tile t+2 in flight across the barrier.  The tile's scales, bias and row factors
+// go to LDS at the tile's start.
+#include "common.h"
+#include "kernels.h"
+
+namespace tone {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void barrier_lds() {   // keeps LDS-DMA in flight (no vmcnt(0) fence)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+__device__ __forceinline__ float fsig(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+
+// E8M0 exponent of an MX block from its max |v|: E = floor(log2 amax) - 8 (biased by 127, clamped)
+__device__ __forceinline__ int mx_exp(float amax) {
+  const int e = (int)((__float_as_uint(amax) >> 23) & 0xff);   // biased exponent of amax (0 for 0/subnormal)
+  return max(0, min(254, e - 8));
+}
+// v / 2^(E - 127) clamped to e4m3's range, two values packed into the low / high half of `w`
+template <bool HI>
+__device__ __forceinline__ uint32_t cvt_pk(float a, float b, float inv, uint32_t w) {
+  a = fminf(fmaxf(a * inv, -448.f), 448.f);
+  b = fminf(fmaxf(b * inv, -448.f), 448.f);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, (int)w, HI);
+}
+__device__ __forceinline__ float exp2i(int ebiased) {   // 2^(127 - ebiased): the inverse block scale
+  return __uint_as_float((uint32_t)(254 - ebiased) << 23);
+}
+// 8 floats -> 8 e4m3 bytes with the block's inverse scale
+__device__ __forceinline__ u32x2 quant8(const float (&v)[8], float inv) {
+  uint32_t w0 = cvt_pk<false>(v[0], v[1], inv, 0u);
+  w0 = cvt_pk<true>(v[2], v[3], inv, w0);
+  uint32_t w1 = cvt_pk<false>(v[4], v[5], inv, 0u);
+  w1 = cvt_pk<true>(v[6], v[7], inv, w1);
+  return u32x2{w0, w1};
+}
+
+}  // namespace
+
+// ---- activation quantization: bf16 [M][K] -> e4m3 [M][K] + E8M0 [M][K/32] (+ 1/(rms + eps)) -------
+// one wave per row, 8 values per lane per pass; the four lanes of a 32-block reduce their max with two
+// xor shuffles.  inv (optional): 1 / (||x||_2 / sqrt(K) + 1e-8), the folded RMSNorm row factor.
+__global__ void __launch_bounds__(256) quant_mx_kernel(const uint16_t* __restrict__ X, int64_t ldx, int M, int K,
+                                                       uint8_t* __restrict__ Q, uint8_t* __restrict__ S,
+                                                       float* __restrict__ inv) {
+  const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;                                    // wave-uniform
+  const uint16_t* x = X + (int64_t)row * ldx;
+  float ss = 0.f;
+  for (int c0 = 0; c0 < K / 8; c0 += 64) {
+    const int c = c0 + lane;
+    const bool on = c < K / 8;
+    u32x4 u = {0u, 0u, 0u, 0u};
+    if (on) u = *reinterpret_cast<const u32x4*>(x + 8 * c);
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+    float am = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      am = fmaxf(am, fabsf(v[i]));
+      ss = fmaf(v[i], v[i], ss);
+    }
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    const int e = mx_exp(am);
+    const u32x2 q = quant8(v, exp2i(e));
+    if (on) {
+      *reinterpret_cast<u32x2*>(Q + (int64_t)row * K + 8 * c) = q;
+      if ((c & 3) == 0) S[(int64_t)row * (K / 32) + c / 4] = (uint8_t)e;
+    }
+  }
+  if (inv) {
+    ss = wave_sum(ss);
+    if (lane == 0) inv[row] = 1.0f / (sqrtf(ss) * rsqrtf((float)K) + kRmsEps);
+  }
+}
+
+hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t* Q, uint8_t* S, float* inv,
+                           hipStream_t st) {
+  if (K % 32 || M <= 0 || ldx % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(quant_mx_kernel, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, M, K, Q, S, inv);
+  return hipGetLastError();
+}
+
+namespace {
+
+constexpr int kMxKB = kDff / 32;   // largest K / 32 (FFN down: 48 scale bytes per row)
+
+// the fragment of row r is 16-byte chunks (l >> 4) and 4 + (l >> 4) of its 128-byte line: the bf16
+// kernels' slot ^= (r >> 1) & 7 makes both ds_read_b128 conflict-free
+__device__ __forceinline__ int mx_swz(int r) { return (r >> 1) & 7; }
+
+template <int BNW, int EPI, bool RS>
+__global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
+  constexpr int BK = 128, QB = 128 * BK, NQW = BNW / 128, STG = (NQW + 2) * QB;
+  constexpr int TI = BNW / 32, TH = TI / 2;                  // n-tiles per wave, per phase half
+  constexpr bool PAIRED = (EPI == EPI_SWIGLU);
+  static_assert(EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU, "STORE/RESID/SWIGLU");
+  // ONE LDS object: ring | W scales [BNW][48] | X scales [256][48] | bias [BNW] | row factors [256]
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG + (BNW + 256) * kMxKB + 4 * (BNW + 256)];
+  uint8_t* sW = lds + 2 * STG;
+  uint8_t* sX = sW + BNW * kMxKB;
+  float* sb = reinterpret_cast<float*>(sX + 256 * kMxKB);
+  float* sr = sb + BNW;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid >> 2, wm = wid & 3, l15 = lane & 15, lg = lane >> 4, g = mx_swz(l15);
+  const int ntn = p.N / BNW, ntm = (p.M + 255) >> 8, ntiles = ntn * ntm;
+  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int q = (ntiles + 7) >> 3, tbeg = xcd * q, tend = min(ntiles, tbeg + q);
+  const int nmine = (tbeg + jb < tend) ? (tend - tbeg - jb + nxb - 1) / nxb : 0;
+  if (nmine <= 0) return;                                       // workgroup-uniform
+  const int nk = p.K / BK, KB = p.K / 32, G = nmine * nk;
+
+  auto tile_of = [&](int u, int& m0, int& n0) {
+    const int t = tbeg + jb + (u / nk) * nxb;
+    m0 = (t / ntn) << 8;
+    n0 = (t % ntn) * BNW;
+  };
+  // quarter j of K-tile u: W rows 128 j.. (j < NQW) or X rows 128 (j - NQW)..; pieces of 8 rows x 128 B
+  auto issue = [&](int u, int j) {
+    int m0, n0;
+    tile_of(u, m0, n0);
+    const int k0 = (u % nk) * BK;
+    uint8_t* dst = lds + (u & 1) * STG + j * QB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int piece = 2 * wid + h, row = piece * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ mx_swz(row);
+      const uint8_t* src = (j < NQW) ? p.W + (int64_t)(n0 + 128 * j + row) * p.K + k0 + 16 * c
+                                     : p.A + (int64_t)min(m0 + 128 * (j - NQW) + row, p.M - 1) * p.lda + k0 + 16 * c;
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, dst + piece * 8 * BK, 16, 0, 0);
+#else
+      (void)src;
+      (void)dst;
+#endif
+    }
+  };
+  auto issue_kt = [&](int u, int from, int to) {   // quarters [from, to) of K-tile u (NQW + 2 per K-tile)
+    for (int j = from; j < to; ++j) issue(u, j);
+  };
+  // per-tile side data: scales, bias, row factors (plain loads; at tile boundaries only)
+  auto load_side = [&](int u) {
+    int m0, n0;
+    tile_of(u, m0, n0);
+    for (int i = tid; i < BNW * KB; i += 512) {
+      const int r = i / KB, c = i % KB;
+      sW[r * kMxKB + c] = p.Ws[(int64_t)(n0 + r) * KB + c];
+    }
+    for (int i = tid; i < 256 * KB; i += 512) {
+      const int r = i / KB, c = i % KB;
+      sX[r * kMxKB + c] = p.As[(int64_t)min(m0 + r, p.M - 1) * p.ldas + c];
+    }
+    for (int i = tid; i < BNW; i += 512) sb[i] = p.bias ? p.bias[n0 + i] : 0.f;
+    if constexpr (RS)
+      for (int i = tid; i < 256; i += 512) sr[i] = p.rs_inv[min(m0 + i, p.M - 1)];
+  };
+
+  const uint8_t* wq = lds + (wn * BNW / 2 / 128) * QB + ((wn * BNW / 2) % 128) * BK;   // wave's W rows
+  const uint8_t* xq = lds + (NQW + (wm >> 1)) * QB + (wm & 1) * 64 * BK;
+  const int wrow0 = wn * BNW / 2, xrow0 = wm * 64;
+  auto rd = [&](const uint8_t* qb, int buf, int tile) {
+    const uint8_t* r = qb + buf * STG + (16 * tile + l15) * BK;
+    const u32x4 a = *reinterpret_cast<const u32x4*>(r + 16 * (lg ^ g));
+    const u32x4 b = *reinterpret_cast<const u32x4*>(r + 16 * ((4 + lg) ^ g));
+    return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+  };
+
+  f32x4 acc[TI][4];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  auto epilogue = [&](int u) {
+    int m0, n0;
+    tile_of(u, m0, n0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ml = xrow0 + 16 * j + l15, m = m0 + ml;
+      const bool ok = m < p.M;
+      const int64_t mrow = min(m, p.M - 1);
+      const float inv = RS ? sr[ml] : 1.0f;
+      if constexpr (PAIRED) {
+        // W rows interleaved in 32-row blocks (g | u); tiles ig, ig + 1 (g) pair with ig + 2, ig + 3 (u)
+#pragma unroll
+        for (int pb = 0; pb < TI / 4; ++pb) {
+          float o[2][4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int ig = 4 * pb + h, nl = wrow0 + 16 * ig + 4 * lg;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gg = fmaf(acc[ig][j][r], inv, sb[nl + r]);
+              const float uu = fmaf(acc[ig + 2][j][r], inv, sb[nl + 32 + r]);
+              o[h][r] = gg * fsig(gg) * uu;
+            }
+          }
+          // lanes lg = 0..3 of this row hold the 32-column MX block: swap so each holds 8 contiguous
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[0][r]), __float_as_uint(o[1][r]), false, false);
+            v[r] = __uint_as_float(sw[0]);
+            v[4 + r] = __uint_as_float(sw[1]);
+          }
+          float am = 0.f;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
+          am = fmaxf(am, __shfl_xor(am, 16, 64));
+          am = fmaxf(am, __shfl_xor(am, 32, 64));
+          const int e = mx_exp(am);
+          const u32x2 qv = quant8(v, exp2i(e));
+          const int blk = (n0 >> 1) + (wrow0 >> 1) + 32 * pb;     // first output column of the block
+          if (ok) {
+            *reinterpret_cast<u32x2*>(p.C8 + mrow * p.ldc + blk + 16 * (lg & 1) + 8 * (lg >> 1)) = qv;
+            if (lg == 0) p.C8s[mrow * p.ldc8s + blk / 32] = (uint8_t)e;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int nl = wrow0 + 16 * i + 4 * lg;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[i][j][r], inv, sb[nl + r]);
+          if constexpr (EPI == EPI_RESID) {
+            const f32x4 rr = *reinterpret_cast<const f32x4*>(p.R + mrow * p.ldr + n0 + nl);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = rr[r] + p.alpha * v[r];
+          }
+          if (EPI == EPI_RESID || !p.c_bf16) {
+            const f32x4 w = {v[0], v[1], v[2], v[3]};
+            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + n0 + nl) = w;
+          }
+          if ((EPI == EPI_STORE && p.c_bf16) || p.C2) {
+            uint16_t* dst = (EPI == EPI_STORE && p.c_bf16) ? static_cast<uint16_t*>(p.C) : p.C2;
+            const __bf16 b0 = (__bf16)v[0], b1 = (__bf16)v[1], b2 = (__bf16)v[2], b3 = (__bf16)v[3];
+            const u32x2 w = {(uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16),
+                             (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16)};
+            if (ok) *reinterpret_cast<u32x2*>(dst + mrow * p.ldc + n0 + nl) = w;
+          }
+        }
+      }
+    }
+  };
+
+  zero();
+  load_side(0);
+  __syncthreads();                                              // side data visible; no DMA in flight yet
+  constexpr int QPT = NQW + 2;                                  // quarters per K-tile
+  // prologue: K-tile 0 whole, the first half of K-tile 1's quarters
+  issue_kt(0, 0, QPT);
+  if (G > 1) {
+    issue_kt(1, 0, QPT / 2);
+    if constexpr (QPT / 2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier_lds();
+  for (int t = 0; t < G; ++t) {
+    const int buf = t & 1, kt = t % nk;
+    i32x8 xf[4], wa[TH], wb[TH];
+    int xs[4], wsa[TH], wsb[TH];
+    // phase 0: every X fragment + the first half of the W tiles
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xf[j] = rd(xq, buf, j);
+      xs[j] = sX[(xrow0 + 16 * j + l15) * kMxKB + 4 * kt + lg];
+    }
+#pragma unroll
+    for (int i = 0; i < TH; ++i) {
+      wa[i] = rd(wq, buf, i);
+      wsa[i] = sW[(wrow0 + 16 * i + l15) * kMxKB + 4 * kt + lg];
+    }
+    if (t + 1 < G) issue_kt(t + 1, QPT / 2, QPT / 2 + (QPT - QPT / 2 + 1) / 2);
+#pragma unroll
+    for (int i = 0; i < TH; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
+    // phase 1: the second half of the W tiles (the stage's last reads)
+#pragma unroll
+    for (int i = 0; i < TH; ++i) {
+      wb[i] = rd(wq, buf, TH + i);
+      wsb[i] = sW[(wrow0 + 16 * (TH + i) + l15) * kMxKB + 4 * kt + lg];
+    }
+    if (t + 1 < G) issue_kt(t + 1, QPT / 2 + (QPT - QPT / 2 + 1) / 2, QPT);
+#pragma unroll
+    for (int i = 0; i < TH; ++i)
+#pragma unroll
+      for (int j = 2; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
+    barrier_lds();                                              // every wave's reads of stage buf done
+    // phase 2
+    if (t + 2 < G) issue_kt(t + 2, 0, (QPT / 2 + 1) / 2);
+#pragma unroll
+    for (int i = 0; i < TH; ++i)
+#pragma unroll
+      for (int j = 2; j < 4; ++j)
+        acc[TH + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
+    // phase 3
+    if (t + 2 < G) issue_kt(t + 2, (QPT / 2 + 1) / 2, QPT / 2);
+#pragma unroll
+    for (int i = 0; i < TH; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[TH + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
+    // K-tile t+1 landed; the first half of K-tile t+2's quarters (2 pieces each) stays in flight
+    if (t + 2 < G) {
+      if constexpr (QPT / 2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier_lds();
+    if (kt == nk - 1) {
+      epilogue(t);
+      zero();
+      if (t + 1 < G) {
+        __syncthreads();                                        // every epilogue done with the side data
+        load_side(t + 1);
+        __syncthreads();
+      }
+    }
+  }
+}
+
+template <int BNW, int EPI>
+hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
+  const int ntiles = (a.N / BNW) * ((a.M + 255) / 256);
+  int grid = 256;
+  const int need = ((ntiles + 7) / 8) * 8;
+  if (grid > need) grid = need;
+  if (a.rs_inv) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true>), dim3(grid), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false>), dim3(grid), dim3(512), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st) {
+  // 128 W rows per tile: the 256-row tile needs 96 fragment VGPRs per wave at 32 bytes per lane and
+  // spills at two waves per SIMD
+  if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || (a.ldc % 8) || a.N % 128) return hipErrorInvalidValue;
+  switch (epi) {
+    case EPI_SWIGLU: return (!a.C8 || !a.C8s) ? hipErrorInvalidValue : launch_mx<128, EPI_SWIGLU>(a, st);
+    case EPI_STORE: return launch_mx<128, EPI_STORE>(a, st);
+    case EPI_RESID: return launch_mx<128, EPI_RESID>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tone

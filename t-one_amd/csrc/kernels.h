@@ -47,6 +47,34 @@ struct GemmArgs {
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
+
+// ---- MXFP8 (TONE_PRECISION_FP8; gemm_mx.hip) --------------------------------------------------------
+// e4m3 values with one E8M0 scale per 32 consecutive values along K (OCP MX)
+struct MxArgs {
+  const uint8_t* A;       // e4m3 [M][K] (lda bytes)
+  int64_t lda;
+  const uint8_t* As;      // E8M0 [M][K/32] (ldas bytes)
+  int64_t ldas;
+  const uint8_t* W;       // e4m3 [N][K]
+  const uint8_t* Ws;      // E8M0 [N][K/32]
+  const float* rs_inv;    // folded RMSNorm: per-row factor 1/(rms + eps) (quant_mx), or nullptr
+  const float* bias;      // [N] or nullptr
+  void* C;                // STORE: fp32, or bf16 when c_bf16; RESID: fp32 (may alias R)
+  int64_t ldc;            // elements (C, C2) / bytes (C8)
+  int c_bf16;
+  const float* R;         // RESID: C = R + alpha * (.)
+  int64_t ldr;
+  float alpha;
+  uint16_t* C2;           // optional bf16 shadow of an fp32 C
+  uint8_t* C8;            // SWIGLU: output as e4m3 [M][N/2] ...
+  uint8_t* C8s;           // ... with E8M0 scales [M][N/64]
+  int64_t ldc8s;
+  int M, N, K;
+};
+hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st);
+// bf16 [M][K] (ldx elements) -> e4m3 [M][K] + E8M0 [M][K/32]; inv (optional): 1/(||row||/sqrt(K) + 1e-8)
+hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t* Q, uint8_t* S, float* inv,
+                           hipStream_t st);
 // bf16 operands, fixed tile/stage variant (microbenchmarks)
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // persistent transposed-orientation bf16 GEMM (gemm_t.hip); variant = tile shape, see there

@@ -7,6 +7,7 @@
 // M = batch * frames.  The step can be captured once per (batch, I/O pointers) into a hipGraph.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -40,7 +41,14 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+// MXFP8 weight (fp8 mode): e4m3 [N][K] + E8M0 scales [N][K/32]
+struct MxW {
+  uint8_t* q = nullptr;
+  uint8_t* s = nullptr;
+};
+
 struct LayerW {
+  MxW mx13[2], mx2[2], mxqkv, mxq, mxkv;   // fp8 mode: the q/k/v and FFN weights as MXFP8
   void* w13[2];       // [3072][384] SwiGLU-interleaved, norm folded
   float* b13[2];
   void* w2[2];        // [384][1536]
@@ -96,6 +104,8 @@ struct tone_session {
   float *wave, *power, *feats, *rA, *rB, *qkv, *kvp, *g, *probs;
   void *x2, *flat, *h, *ctx, *d, *xn, *kv, *yred;   // bf16 in bf16 mode
   uint16_t *xbA, *xbB;                              // bf16 shadows of rA / rB (bf16 mode)
+  uint8_t *a8 = nullptr, *a8s = nullptr, *h8 = nullptr, *h8s = nullptr;   // fp8 mode: MXFP8 GEMM inputs
+  float* inv8 = nullptr;                            // fp8 mode: folded-RMSNorm row factors of a8
   float *ws, *ws_ss;
   int64_t ws_cap = 0;
 
@@ -162,11 +172,59 @@ float bf2f(uint16_t h) {
   return f;
 }
 
+// bf16 activations and GEMM operands: bf16 mode, and fp8 mode (bf16 everywhere except the MXFP8 GEMMs)
+bool bfmode(const tone_session* s) {
+  return s->precision == TONE_PRECISION_BF16 || s->precision == TONE_PRECISION_FP8;
+}
+
+// OCP e4m3fn, round to nearest even, saturating at 448 (0x7E; 0x7F is NaN)
+uint8_t f32_to_e4m3(float x) {
+  const uint8_t sg = std::signbit(x) ? 0x80 : 0;
+  const float a = std::fabs(x);
+  if (std::isnan(x)) return 0x7F;
+  if (a >= 448.0f) return sg | 0x7E;
+  if (a < 0.015625f) {                                   // below 2^-6: subnormal, step 2^-9
+    const float m = std::nearbyint(a * 512.0f);          // default rounding mode: to nearest even
+    return sg | (uint8_t)m;                              // m == 8 encodes 2^-6 (exp 1, mant 0)
+  }
+  int ex;
+  const float f = std::frexp(a, &ex);                    // a = f 2^ex, f in [0.5, 1)
+  int e = ex - 1;
+  int m = (int)std::nearbyint((f * 2.0f - 1.0f) * 8.0f);
+  if (m == 8) { m = 0; ++e; }
+  if (e > 8 || (e == 8 && m == 7)) return sg | 0x7E;
+  return sg | (uint8_t)(((e + 7) << 3) | m);
+}
+
+// MXFP8 upload (fp8 mode): per 32 consecutive values along K, E = floor(log2 max|w|) - 8 (E8M0, biased),
+// values w / 2^(E - 127) in e4m3 -- the same rule as quant_mx_kernel (gemm_mx.hip)
+int upload_mx(tone_session* s, MxW* out, const std::vector<float>& v, int N, int K) {
+  std::vector<uint8_t> q((size_t)N * K), sc((size_t)N * K / 32);
+  for (int n = 0; n < N; ++n)
+    for (int b = 0; b < K / 32; ++b) {
+      const float* w = v.data() + (size_t)n * K + 32 * b;
+      float am = 0.f;
+      for (int i = 0; i < 32; ++i) am = std::fmax(am, std::fabs(w[i]));
+      uint32_t bits;
+      std::memcpy(&bits, &am, 4);
+      const int e = std::max(0, std::min(254, (int)((bits >> 23) & 0xff) - 8));
+      sc[(size_t)n * (K / 32) + b] = (uint8_t)e;
+      const float inv = std::ldexp(1.0f, 127 - e);
+      for (int i = 0; i < 32; ++i) q[(size_t)n * K + 32 * b + i] = f32_to_e4m3(w[i] * inv);
+    }
+  int rc = dalloc(s, &out->q, q.size());
+  if (!rc) rc = dalloc(s, &out->s, sc.size());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(out->q, q.data(), q.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(out->s, sc.data(), sc.size(), hipMemcpyHostToDevice));
+  return TONE_OK;
+}
+
 // GEMM weight in the session's precision (fp32, or bf16 bits).  fp32 (split) mode also uploads the
 // exact three-term bf16 split [3][N][K] (w = w0 + w1 + w2, each term the bf16 rounding of what the
 // previous ones leave) that gemm_x3 reads.
 int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
-  if (s->precision != TONE_PRECISION_BF16) {
+  if (!bfmode(s)) {
     float* p;
     int rc = upload(s, &p, v);
     *out = p;
@@ -332,7 +390,7 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   a.ws_ss = s->ws_ss;
   a.ws_cap = s->ws_cap;
   a.k_split = 0;
-  const bool bf = s->precision == TONE_PRECISION_BF16;
+  const bool bf = bfmode(s);
   a.a_bf16 = bf && a_bf16;
   a.c_bf16 = bf && c_bf16;
   a.C2 = bf ? c2 : nullptr;
@@ -340,7 +398,38 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
     auto it = s->w3.find(W);
     a.W3 = it == s->w3.end() ? nullptr : it->second;
   }
-  LAUNCH(fam, gemm(a, epi, s->precision == TONE_PRECISION_BF16, st));
+  LAUNCH(fam, gemm(a, epi, bf, st));
+  return TONE_OK;
+}
+
+// fp8 mode: one MXFP8 GEMM (gemm_mx.hip); A8/As the e4m3 rows and their scales (K bytes / K/32 per row)
+int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8, const uint8_t* As, const MxW& w, void* C,
+            int64_t ldc, const float* bias, int M, int N, int K, int epi, const float* inv, const float* R = nullptr,
+            float alpha = 1.0f, bool c_bf16 = false, uint16_t* C2 = nullptr, uint8_t* C8 = nullptr,
+            uint8_t* C8s = nullptr) {
+  MxArgs a{};
+  a.A = A8;
+  a.lda = K;
+  a.As = As;
+  a.ldas = K / 32;
+  a.W = w.q;
+  a.Ws = w.s;
+  a.rs_inv = inv;
+  a.bias = bias;
+  a.C = C;
+  a.ldc = ldc;
+  a.c_bf16 = c_bf16;
+  a.R = R;
+  a.ldr = ldc;
+  a.alpha = alpha;
+  a.C2 = C2;
+  a.C8 = C8;
+  a.C8s = C8s;
+  a.ldc8s = N / 64;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  LAUNCH(fam, gemm_mx(a, epi, st));
   return TONE_OK;
 }
 
@@ -360,7 +449,7 @@ const void* act_at(const float* base, int64_t i, bool bf) {
 // bf16 shadow written by each of its producers; the other operands are produced in bf16 directly.
 int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* logp, int B, hipStream_t st) {
   const int D = kD;
-  const bool bf = s->precision == TONE_PRECISION_BF16;
+  const bool bf = bfmode(s), f8 = s->precision == TONE_PRECISION_FP8;
   uint16_t* shA = bf ? s->xbA : nullptr;
   uint16_t* shB = bf ? s->xbB : nullptr;
   LAUNCH("mel_prep", launch_mel_prep(signal, sr, s->wave, B, st));
@@ -380,10 +469,22 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     const int M = B * T;
     const void* xa = bf ? static_cast<const void*>(xs) : x;   // A operand of the rowscale GEMMs
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
-    CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[0], s->h, kDff, w.b13[0], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
-                   1.0f, true, true));
-    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[0], x, D, w.b2[0], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
-                   false, xs));
+    // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
+    // up-projection's epilogue
+    auto ffn = [&](int f) -> int {
+      if (f8) {
+        LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->inv8, st));
+        CALL(mx_call(s, st, "gemm_ffn_up", s->a8, s->a8s, w.mx13[f], nullptr, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU,
+                     s->inv8, nullptr, 1.0f, false, nullptr, s->h8, s->h8s));
+        return mx_call(s, st, "gemm_ffn_down", s->h8, s->h8s, w.mx2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, nullptr, x,
+                       0.5f, false, xs);
+      }
+      CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[f], s->h, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
+                     1.0f, true, true));
+      return gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
+                       false, xs);
+    };
+    CALL(ffn(0));
     // MHSA (conformer_blocks.py:816-825)
     AttnArgs aa{};
     aa.ctx = s->ctx;
@@ -402,8 +503,14 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       const bool rec = (l == 0 || l == 7);
       const int N = rec ? 3 * D : D;
       // q/k/v in bf16 in bf16 mode (half the attention kernel's input bytes)
-      CALL(gemm_call(s, st, "gemm_qkv", xa, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1, nullptr, 1.0f, true,
-                     bf));
+      if (f8) {
+        LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->inv8, st));
+        CALL(mx_call(s, st, "gemm_qkv", s->a8, s->a8s, w.mxqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, s->inv8, nullptr,
+                     1.0f, true));
+      } else {
+        CALL(gemm_call(s, st, "gemm_qkv", xa, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1, nullptr, 1.0f, true,
+                       bf));
+      }
       aa.S = 0;
       aa.recompute = rec;
       aa.reduced = 0;
@@ -417,10 +524,20 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     } else {
       const int S = (l == 14) ? kMhsaS / 2 : kMhsaS;
       LAUNCH("kv_assemble", launch_kv_assemble(x, w.norm_att, sr, l - 14, T, S, s->xn, s->kv, bf, B, st));
-      CALL(gemm_call(s, st, "gemm_qkv", s->xn, D, w.wq, s->qkv, D, w.bq, M, D, D, EPI_STORE, 0, nullptr, 1.0f, true,
-                     bf));
-      CALL(gemm_call(s, st, "gemm_qkv", s->kv, D, w.wkv, s->kvp, 2 * D, w.bkv, B * (S + T), 2 * D, D, EPI_STORE, 0,
-                     nullptr, 1.0f, true, bf));
+      if (f8) {
+        const int MK = B * (S + T);
+        LAUNCH("quant_mx", launch_quant_mx(static_cast<const uint16_t*>(s->xn), D, M, D, s->a8, s->a8s, nullptr, st));
+        CALL(mx_call(s, st, "gemm_qkv", s->a8, s->a8s, w.mxq, s->qkv, D, w.bq, M, D, D, EPI_STORE, nullptr, nullptr, 1.0f,
+                     true));
+        LAUNCH("quant_mx", launch_quant_mx(static_cast<const uint16_t*>(s->kv), D, MK, D, s->a8, s->a8s, nullptr, st));
+        CALL(mx_call(s, st, "gemm_qkv", s->a8, s->a8s, w.mxkv, s->kvp, 2 * D, w.bkv, MK, 2 * D, D, EPI_STORE, nullptr,
+                     nullptr, 1.0f, true));
+      } else {
+        CALL(gemm_call(s, st, "gemm_qkv", s->xn, D, w.wq, s->qkv, D, w.bq, M, D, D, EPI_STORE, 0, nullptr, 1.0f, true,
+                       bf));
+        CALL(gemm_call(s, st, "gemm_qkv", s->kv, D, w.wkv, s->kvp, 2 * D, w.bkv, B * (S + T), 2 * D, D, EPI_STORE, 0,
+                       nullptr, 1.0f, true, bf));
+      }
       aa.S = S;
       aa.recompute = 1;
       aa.reduced = (l == 14);
@@ -436,10 +553,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st));
     CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
     // FFN2 + norm_out (conformer_blocks.py:832-836)
-    CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[1], s->h, kDff, w.b13[1], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
-                   1.0f, true, true));
-    CALL(gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[1], x, D, w.b2[1], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
-                   false, xs));
+    CALL(ffn(1));
     LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
       LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, st));
@@ -522,7 +636,7 @@ int finalize_weights(tone_session* s) {
       sh[c] = (float)(((double)(*c1b)[c] - (double)(*bn1[2])[c]) * scale + (double)(*bn1[1])[c]);
     }
     CALL(upload(s, &s->w1, *c1w));
-    if (s->precision == TONE_PRECISION_BF16) {
+    if (bfmode(s)) {
       std::vector<float> wt((size_t)kSub1Kt * kSub1C * 32, 0.f);
       for (int c = 0; c < kSub1C; ++c)
         for (int kt = 0; kt < kSub1Kt; ++kt)
@@ -540,7 +654,7 @@ int finalize_weights(tone_session* s) {
       sh[c] = (float)(((double)(*c2b)[c] - (double)(*bn2[2])[c]) * scale + (double)(*bn2[1])[c]);
     }
     // conv2 weight tap-major [c2][kt][kf][ci] for the implicit GEMM over channels-last input
-    const int kw = s->precision == TONE_PRECISION_BF16 ? kConv2KPad : kConv2K;   // bf16: zero pad tap
+    const int kw = bfmode(s) ? kConv2KPad : kConv2K;   // bf16: zero pad tap
     std::vector<float> w2r((size_t)64 * kw, 0.f);
     for (int c2 = 0; c2 < 64; ++c2)
       for (int ci = 0; ci < 32; ++ci)
@@ -606,6 +720,10 @@ int finalize_weights(tone_session* s) {
       CALL(upload_w(s, &lw.w13[f], w13));
       CALL(upload(s, &lw.b13[f], b13));
       CALL(upload_w(s, &lw.w2[f], *w2));
+      if (s->precision == TONE_PRECISION_FP8) {
+        CALL(upload_mx(s, &lw.mx13[f], w13, 2 * kDff, D));
+        CALL(upload_mx(s, &lw.mx2[f], *w2, D, kDff));
+      }
       CALL(upload(s, &lw.b2[f], *b2));
     }
     const std::string a = p + "self_attn.";
@@ -643,6 +761,7 @@ int finalize_weights(tone_session* s) {
         }
       }
       CALL(upload_w(s, &lw.wqkv, wqkv));
+      if (s->precision == TONE_PRECISION_FP8) CALL(upload_mx(s, &lw.mxqkv, wqkv, nb * D, D));
       CALL(upload(s, &lw.bqkv, bqkv));
     } else {
       std::vector<float> wkv((size_t)2 * D * D), bkv(2 * D);
@@ -653,6 +772,10 @@ int finalize_weights(tone_session* s) {
       CALL(upload_w(s, &lw.wq, *wq));
       CALL(upload(s, &lw.bq, *bq));
       CALL(upload_w(s, &lw.wkv, wkv));
+      if (s->precision == TONE_PRECISION_FP8) {
+        CALL(upload_mx(s, &lw.mxq, *wq, D, D));
+        CALL(upload_mx(s, &lw.mxkv, wkv, 2 * D, D));
+      }
       CALL(upload(s, &lw.bkv, bkv));
       CALL(upload(s, &lw.norm_att, *natt));
     }
@@ -718,6 +841,13 @@ int finalize_weights(tone_session* s) {
   CALL(dalloc(s, reinterpret_cast<float**>(&s->yred), MB * (kT / 2) * 4 * D));
   CALL(dalloc(s, &s->xbA, MB * kT * D));
   CALL(dalloc(s, &s->xbB, MB * (kT / 2) * D));
+  if (s->precision == TONE_PRECISION_FP8) {
+    CALL(dalloc(s, &s->a8, MB * 40 * D));            // the largest quantized input: layer 15's k/v rows
+    CALL(dalloc(s, &s->a8s, MB * 40 * (D / 32)));
+    CALL(dalloc(s, &s->inv8, MB * 40));
+    CALL(dalloc(s, &s->h8, MB * kT * kDff));
+    CALL(dalloc(s, &s->h8s, MB * kT * (kDff / 32)));
+  }
   // split-K workspace: only small batches split (large ones fill the chip with whole-K tiles)
   s->ws_cap = 16ll << 20;
   CALL(dalloc(s, &s->ws, (size_t)s->ws_cap));
@@ -797,7 +927,8 @@ const char* tone_last_error(void) { return g_err.c_str(); }
 
 int tone_session_create(tone_session** out, int device, int precision, int max_batch) {
   if (!out) return fail(TONE_E_INVALID, "null out pointer");
-  if (precision != TONE_PRECISION_FP32 && precision != TONE_PRECISION_BF16 && precision != TONE_PRECISION_FP32_MFMA)
+  if (precision != TONE_PRECISION_FP32 && precision != TONE_PRECISION_BF16 && precision != TONE_PRECISION_FP32_MFMA &&
+      precision != TONE_PRECISION_FP8)
     return fail(TONE_E_INVALID, "unknown precision " + std::to_string(precision));
   if (max_batch <= 0) return fail(TONE_E_INVALID, "max_batch must be positive");
   int n = 0;

@@ -93,6 +93,92 @@ __global__ void err_kernel(const void* C, int cbf, const float* ref, int64_t n, 
   atomicMax(reinterpret_cast<int*>(err), __float_as_int(e));
 }
 
+// MXFP8 helpers (variant 99): dequantize e4m3 + E8M0 to fp32, reference with a given row factor
+__global__ void dequant_mx_kernel(const uint8_t* Q, const uint8_t* S, float* out, int64_t rows, int K) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * K) return;
+  const int64_t r = i / K;
+  const int k = (int)(i % K);
+  const float sc = __uint_as_float((uint32_t)S[r * (K / 32) + k / 32] << 23);
+  out[i] = __builtin_amdgcn_cvt_f32_fp8((int)Q[i], 0) * sc;
+}
+__global__ void ref_mx_kernel(const float* A, const float* W, const float* bias, const float* R, const float* inv,
+                              float* out, int M, int N, int K, int epi) {
+  const int m = blockIdx.y, o = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nout = (epi >= 2) ? N / 2 : N;
+  if (o >= nout) return;
+  const double f = inv ? inv[m] : 1.0;
+  auto dot = [&](int n) {
+    double acc = 0.0;
+    for (int k = 0; k < K; ++k) acc += (double)A[(int64_t)m * K + k] * W[(int64_t)n * K + k];
+    return acc * f + bias[n];
+  };
+  double v;
+  if (epi <= 1) {
+    v = dot(o);
+    if (epi == 1) v = R[(int64_t)m * N + o] + v;
+  } else {
+    const int blk = o / 32, c = o % 32, n0 = blk * 64 + c;
+    const double g = dot(n0), u = dot(n0 + 32);
+    v = g / (1.0 + exp(-g)) * u;
+  }
+  out[(int64_t)m * nout + o] = (float)v;
+}
+
+static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, const float* R, float* ref, float* err,
+                   int M, int N, int K, int epi, int rowscale, int iters) {
+  const int nout = epi >= 2 ? N / 2 : N;
+  uint8_t *A8, *As, *W8, *Ws, *C8, *C8s;
+  float *inv, *Af, *Wf, *C, *Cf;
+  CK(hipMalloc(&A8, (size_t)M * K)); CK(hipMalloc(&As, (size_t)M * K / 32));
+  CK(hipMalloc(&W8, (size_t)N * K)); CK(hipMalloc(&Ws, (size_t)N * K / 32));
+  CK(hipMalloc(&inv, (size_t)M * 4)); CK(hipMalloc(&Af, (size_t)M * K * 4)); CK(hipMalloc(&Wf, (size_t)N * K * 4));
+  CK(hipMalloc(&C, (size_t)M * nout * 4)); CK(hipMalloc(&Cf, (size_t)M * nout * 4));
+  CK(hipMalloc(&C8, (size_t)M * nout)); CK(hipMalloc(&C8s, (size_t)M * nout / 32));
+  CK(launch_quant_mx(A, K, M, K, A8, As, rowscale ? inv : nullptr, 0));
+  CK(launch_quant_mx(W, K, N, K, W8, Ws, nullptr, 0));
+  hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)M * K + 255) / 256)), dim3(256), 0, 0, A8, As, Af, (int64_t)M, K);
+  hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)N * K + 255) / 256)), dim3(256), 0, 0, W8, Ws, Wf, (int64_t)N, K);
+  hipLaunchKernelGGL(ref_mx_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, Af, Wf, bias, R, rowscale ? inv : nullptr,
+                     ref, M, N, K, epi);
+  MxArgs a{};
+  a.A = A8; a.lda = K; a.As = As; a.ldas = K / 32; a.W = W8; a.Ws = Ws; a.rs_inv = rowscale ? inv : nullptr;
+  a.bias = bias; a.C = C; a.ldc = nout; a.c_bf16 = 0; a.R = R; a.ldr = N; a.alpha = 1.f;
+  a.C8 = C8; a.C8s = C8s; a.ldc8s = nout / 32; a.M = M; a.N = N; a.K = K;
+  if (epi >= 2) a.ldc = nout;   // bytes of C8 rows
+  hipError_t rc = gemm_mx(a, epi, 0);
+  if (rc != hipSuccess) { printf("{\"variant\": 99, \"error\": \"%s\"}\n", hipGetErrorString(rc)); return; }
+  CK(hipDeviceSynchronize());
+  const float* chk = C;
+  if (epi >= 2) {
+    hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)M * nout + 255) / 256)), dim3(256), 0, 0, C8, C8s, Cf, (int64_t)M, nout);
+    chk = Cf;
+  }
+  CK(hipMemset(err, 0, 4));
+  hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)chk, 0, ref, (int64_t)M * nout, err);
+  float herr;
+  CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int i = 0; i < 3; ++i) CK(gemm_mx(a, epi, 0));
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK(gemm_mx(a, epi, 0));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / iters;
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK(launch_quant_mx(A, K, M, K, A8, As, rowscale ? inv : nullptr, 0));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float qms;
+  CK(hipEventElapsedTime(&qms, e0, e1));
+  printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": 99, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"quant_us\": %.2f}\n",
+         M, K, N, epi, us, 2.0 * M * N * (double)K / us * 1e-6, herr, qms * 1e3 / iters);
+  fflush(stdout);
+}
+
 int main(int argc, char** argv) {
   if (argc < 6) { fprintf(stderr, "usage: %s M K N epi v1,v2,.. [nsplit] [iters]\n", argv[0]); return 2; }
   const int M = atoi(argv[1]), K = atoi(argv[2]), N = atoi(argv[3]), epi = atoi(argv[4]);
@@ -175,6 +261,10 @@ int main(int argc, char** argv) {
   char* list = strdup(argv[5]);
   for (char* tok = strtok(list, ","); tok; tok = strtok(nullptr, ",")) {
     const int vv = atoi(tok);
+    if (vv == 99) {   // MXFP8 path: quant_mx + gemm_mx vs an fp64 reference on the dequantized operands
+      run_mx(A, W, bias, R, ref, err, M, N, K, epi, rowscale, iters);
+      continue;
+    }
     // v % 100 = variant (20..23: gemm_t tiles); (v / 100) bits: 1 N-partitioned XCD order,
     // 2 non-temporal stores, 4.. debug (no epilogue / no K loop)
     const int v = vv < 0 ? vv : (vv % 100);   // -1 gemm() bf16, -2 gemm() fp32 (+W3), -3 gemm() fp32 (no W3)

@@ -52,7 +52,9 @@ class TextPhrase:
 
 @dataclass
 class FrameSplitterState:
-    """Frames carried between steps (the reference keeps the logprob rows, logprob_splitter.py:36-40)."""
+    """Frames carried between steps (the reference keeps the logprob rows, logprob_splitter.py:36-40).
+    ``tokens`` is the per-frame payload: greedy tokens (L,) int32, or the logprob rows (L, 35) float32
+    when a host decoder (e.g. the reference's BeamSearchCTCDecoder + KenLM) decodes the phrases."""
     tokens: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
     speech: np.ndarray = field(default_factory=lambda: np.zeros(0, bool))
     offset: int = 0
@@ -96,7 +98,8 @@ def split_frames(tokens: np.ndarray, speech: np.ndarray, state: Optional[FrameSp
                  is_last: bool = False) -> tuple[list[tuple[np.ndarray, int, int]], FrameSplitterState]:
     """One splitter step on frames -> ([(phrase tokens, start_frame, end_frame)], next state)."""
     state = state or FrameSplitterState()
-    toks = np.concatenate([state.tokens, np.asarray(tokens, np.int32)])
+    tokens = np.asarray(tokens)
+    toks = np.concatenate([state.tokens.astype(tokens.dtype, copy=False).reshape((-1,) + tokens.shape[1:]), tokens])
     sp = np.concatenate([state.speech, np.asarray(speech, bool)])
     out, last = [], 0
     for s, e in _phrases(sp, is_last):
@@ -113,9 +116,12 @@ def phrase_times(start_frame: int, end_frame: int) -> tuple[float, float]:
     return st, max(st, round(end_frame * C.FRAME_SIZE - shift, 2))
 
 
-def frames_to_phrases(tokens, speech, state, *, is_last=False) -> tuple[list[TextPhrase], FrameSplitterState]:
+def frames_to_phrases(tokens, speech, state, *, is_last=False, decode=greedy_text
+                      ) -> tuple[list[TextPhrase], FrameSplitterState]:
+    """``decode`` maps a phrase's payload to its text: greedy_text on tokens, or a host decoder's
+    ``forward`` on logprob rows (tone/pipeline.py:147-150 calls ``self.decoder.forward``)."""
     found, state = split_frames(tokens, speech, state, is_last=is_last)
-    return [TextPhrase(greedy_text(t), *phrase_times(s, e)) for t, s, e in found], state
+    return [TextPhrase(decode(t), *phrase_times(s, e)) for t, s, e in found], state
 
 
 class StreamingGreedyPipeline:
@@ -127,11 +133,18 @@ class StreamingGreedyPipeline:
 
     Slot s owns slab rows 2s and 2s+1; ``_parity[s]`` says which one holds its current state.  A
     step reads row 2s + p and writes row 2s + 1 - p for the stepping streams only.
+
+    ``decoder``: optional host decoder with the reference's ``forward(logprobs (L, 35) float32) -> str``
+    (``tone.decoder.BeamSearchCTCDecoder`` -- pyctcdecode + KenLM, BASELINE config 5 -- or
+    ``GreedyCTCDecoder``).  With it the step's logprobs come to the host (1.4 KB per stream-chunk),
+    phrases are still cut by the device speech flags, and each finished phrase's logprob rows go to
+    ``decoder.forward`` exactly as tone/pipeline.py:146-150 does.  Without it the text is the device's
+    greedy tokens (10 ids + 10 bits per stream-chunk cross PCIe).
     """
 
     CHUNK_SIZE = C.AUDIO_CHUNK_SAMPLES
 
-    def __init__(self, session, n_slots: int):
+    def __init__(self, session, n_slots: int, decoder=None):
         import torch
         if n_slots <= 0:
             raise ValueError("n_slots must be positive")
@@ -151,6 +164,15 @@ class StreamingGreedyPipeline:
         self._sig_h = torch.zeros((mb, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32).pin_memory()
         self._rows_h = torch.zeros((2, mb), dtype=torch.int32).pin_memory()
         self._info_h = torch.zeros((mb, C.CHUNK_FRAMES), dtype=torch.int32).pin_memory()
+        self.decoder = decoder
+        self._logp_h = torch.zeros((mb, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32).pin_memory() \
+            if decoder is not None else None
+        self._last_logp: Optional[np.ndarray] = None
+
+    def _fresh_state(self) -> FrameSplitterState:
+        if self.decoder is None:
+            return FrameSplitterState()
+        return FrameSplitterState(tokens=np.zeros((0, C.VOCAB), np.float32))
 
     # --- slots -------------------------------------------------------------------------------
     def open_stream(self) -> int:
@@ -159,7 +181,7 @@ class StreamingGreedyPipeline:
         slot = self._free.pop()
         self._parity[slot] = 0
         self._slab[2 * slot].zero_()          # onnx_wrapper.py:114-115: zero state at stream start
-        self._open[slot] = FrameSplitterState()
+        self._open[slot] = self._fresh_state()
         return slot
 
     def close_stream(self, slot: int) -> None:
@@ -185,6 +207,7 @@ class StreamingGreedyPipeline:
         n = len(slots)
         mb = self.session.max_batch
         info = np.empty((n, C.CHUNK_FRAMES), np.int32)
+        logp = np.empty((n, C.CHUNK_FRAMES, C.VOCAB), np.float32) if self.decoder is not None else None
         self.session.set_frame_info(self._info)    # frame_info is session state: claim it every step
         for b0 in range(0, n, mb):
             b1 = min(n, b0 + mb)
@@ -199,9 +222,14 @@ class StreamingGreedyPipeline:
             self.session.run_rows(self._sig[:nb], self._rows[0, :nb], self._rows[1, :nb], self._slab,
                                   self._logp, check_rows=False)   # rows are built here, distinct by construction
             self._info_h[:nb].copy_(self._info[:nb], non_blocking=True)
+            if logp is not None:
+                self._logp_h[:nb].copy_(self._logp[:nb], non_blocking=True)
             torch.cuda.current_stream(self.session.dev).synchronize()
             info[b0:b1] = self._info_h[:nb].numpy()
+            if logp is not None:
+                logp[b0:b1] = self._logp_h[:nb].numpy()
             self._parity[sl] ^= 1
+        self._last_logp = logp
         return info
 
     def forward(self, chunks: np.ndarray, slots: Sequence[int], is_last: Optional[Sequence[bool]] = None
@@ -223,7 +251,11 @@ class StreamingGreedyPipeline:
         out: list[list[TextPhrase]] = []
         for i, slot in enumerate(slots):
             toks, speech = decode_frame_info(info[i])
-            phrases, self._open[slot] = frames_to_phrases(toks, speech, self._open[slot], is_last=is_last[i])
+            if self.decoder is None:
+                phrases, self._open[slot] = frames_to_phrases(toks, speech, self._open[slot], is_last=is_last[i])
+            else:
+                phrases, self._open[slot] = frames_to_phrases(self._last_logp[i], speech, self._open[slot],
+                                                              is_last=is_last[i], decode=self.decoder.forward)
             out.append(phrases)
         return out
 
@@ -244,6 +276,21 @@ class StreamingGreedyPipeline:
             return phrases
         finally:
             self.close_stream(slot)
+
+
+class GreedyLogprobDecoder:
+    """Host restatement of ``tone.decoder.GreedyCTCDecoder.forward`` (tone/decoder.py:38-59): argmax,
+    collapse repeats, drop the blank.  The stand-in host decoder for tests where pyctcdecode / KenLM
+    (BeamSearchCTCDecoder) are not installed; both take (L, 35) float32 logprob rows."""
+
+    def forward(self, logprobs: np.ndarray) -> str:
+        if not isinstance(logprobs, np.ndarray):
+            raise TypeError(f"Incorrect 'logprobs' type: expected np.ndarray, but got {type(logprobs)}")
+        if logprobs.shape[1:] != (C.VOCAB,):
+            raise ValueError(f"Shape of 'logprobs' must be (L, 35), but got {logprobs.shape}")
+        if logprobs.dtype != np.float32:
+            raise ValueError(f"Incorrect dtype of 'logprobs': expected np.float32, but got {logprobs.dtype}")
+        return greedy_text(logprobs.argmax(axis=-1))
 
 
 class StreamScheduler:

@@ -326,3 +326,37 @@ def test_scheduler_matches_single_stream_decode(session):
                    [(p.text, p.start_time, p.end_time) for p in want]
     finally:
         session.set_frame_info(None)
+
+
+# --------------------------------------------------------------------------- host decoder wiring
+def test_frames_to_phrases_with_host_decoder_matches_greedy():
+    """The logprob-row payload path (for a host beam decoder such as the reference's KenLM
+    BeamSearchCTCDecoder) cuts the same phrases as the token path, and with the greedy host decoder
+    gives the same texts."""
+    rng = np.random.default_rng(5)
+    logp = np.log(rng.dirichlet(np.ones(35) * 0.3, size=(9, 10))).astype(np.float32)
+    speech = rng.random((9, 10)) < 0.6
+    speech[3:6] = False
+    dec = P.GreedyLogprobDecoder()
+    st_t, st_l, got_t, got_l = None, P.FrameSplitterState(tokens=np.zeros((0, 35), np.float32)), [], []
+    for c in range(9):
+        a, st_t = P.frames_to_phrases(logp[c].argmax(-1).astype(np.int32), speech[c], st_t, is_last=c == 8)
+        b, st_l = P.frames_to_phrases(logp[c], speech[c], st_l, is_last=c == 8, decode=dec.forward)
+        got_t += a
+        got_l += b
+    assert got_t == got_l and len(got_t) >= 2
+    with pytest.raises(ValueError):
+        dec.forward(np.zeros((3, 34), np.float32))
+
+
+@pytest.mark.gpu
+def test_host_decoder_pipeline_matches_device_greedy(session):
+    """StreamingGreedyPipeline with a host decoder (logprobs to the host, phrase rows to
+    decoder.forward -- the KenLM wiring) == the device greedy path on the same audio."""
+    audio = _noise_audio()
+    try:
+        want = P.StreamingGreedyPipeline(session, n_slots=1).forward_offline(audio)
+        got = P.StreamingGreedyPipeline(session, n_slots=1, decoder=P.GreedyLogprobDecoder()).forward_offline(audio)
+    finally:
+        session.set_frame_info(None)
+    assert [(p.text, p.start_time, p.end_time) for p in got] == [(p.text, p.start_time, p.end_time) for p in want]

@@ -273,14 +273,21 @@ def test_fp32_split_vs_fp32_mfma(weights, oracle):
 BF16_MAX, BF16_P99, BF16_MARGIN = 0.08, 0.05, 0.1
 
 
-def assert_bf16_close(lp, ref, what=""):
+# fp8 (MXFP8 q/k/v + FFN GEMMs, BASELINE config 5) bounds, measured the same way (PREC=fp8
+# scripts/bf16_measure.py, profiles/r02_fp8_bounds.json): max |dlogp| 0.36-0.43 per chunk, p99 0.27-0.30,
+# argmax 99.8-100 % identical.  Bounds: max 0.6, p99 0.4, argmax identical where the margin exceeds 1.0
+# and >= 99 % overall.
+FP8_MAX, FP8_P99, FP8_MARGIN = 0.6, 0.4, 1.0
+
+
+def assert_bf16_close(lp, ref, what="", bounds=(BF16_MAX, BF16_P99, BF16_MARGIN), agree=0.995):
+    mx, p99, margin = bounds
     d = np.abs(lp - ref)
-    assert d.max() < BF16_MAX and np.percentile(d, 99) < BF16_P99, \
-        f"{what} max {d.max():.3g} p99 {np.percentile(d, 99):.3g}"
+    assert d.max() < mx and np.percentile(d, 99) < p99, f"{what} max {d.max():.3g} p99 {np.percentile(d, 99):.3g}"
     srt = np.sort(ref, axis=-1)
-    clear = (srt[..., -1] - srt[..., -2]) > BF16_MARGIN
+    clear = (srt[..., -1] - srt[..., -2]) > margin
     np.testing.assert_array_equal(lp.argmax(-1)[clear], ref.argmax(-1)[clear], err_msg=f"{what} argmax")
-    assert np.mean(lp.argmax(-1) == ref.argmax(-1)) >= 0.995, what
+    assert np.mean(lp.argmax(-1) == ref.argmax(-1)) >= agree, what
 
 
 def test_bf16_mode_close_to_oracle(weights, oracle):
@@ -350,16 +357,42 @@ def test_bf16_config3_staggered_streams(weights, oracle):
         s.close()
 
 
-def test_bf16_example_audio_greedy_decode(weights, oracle):
-    """Greedy decode of the reference's example utterance in bf16 mode == the oracle decode of the fp32
-    oracle's logprobs (phrases, times and every frame's greedy token)."""
+def test_fp8_staggered_streams(weights, oracle):
+    """BASELINE config 5 arithmetic (MXFP8 q/k/v + FFN GEMMs, everything else as bf16 mode): B = 512, 6
+    stateful chunks with staggered starts, 32 sampled streams against the fp32 oracle's own state chain."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    b, n = 512, 6
+    pick = np.arange(0, b, 16)
+    s = ToneSession(weights, precision="fp8", max_batch=b)
+    rng = np.random.default_rng(37)
+    off = np.arange(b) % 4
+    st = torch.zeros((b, C.STATE_SIZE), dtype=torch.float16, device=s.dev)
+    st_o = np.zeros((len(pick), C.STATE_SIZE), np.float16)
+    try:
+        for c in range(n):
+            pcm = synthetic_pcm(rng, b)
+            st[torch.from_numpy(off == c).to(s.dev)] = 0
+            st_o[off[pick] == c] = 0
+            lp, st = s.step(torch.from_numpy(pcm).to(s.dev), st)
+            lp_o, st_o = oracle.step(pcm[pick], st_o)
+            live = off[pick] <= c
+            assert_bf16_close(lp.cpu().numpy()[pick][live], lp_o[live], f"chunk {c}", (FP8_MAX, FP8_P99, FP8_MARGIN), 0.99)
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp8"])
+def test_low_precision_example_audio_greedy_decode(weights, oracle, prec):
+    """Greedy decode of the reference's example utterance in bf16 / fp8 mode == the oracle decode of the
+    fp32 oracle's logprobs (phrases, times and every frame's greedy token)."""
     _gpu()
     import tone_decode_oracle as O
     from tone_amd.model import ToneSession
     audio = np.load(GOLDEN / "audio_short_pcm.npy").astype(np.int32)
     padded = np.pad(audio, (O.PADDING, O.PADDING))
     padded = np.pad(padded, (0, -len(padded) % 2400)).reshape(-1, 2400)
-    s = ToneSession(weights, precision="bf16", max_batch=1)
+    s = ToneSession(weights, precision=prec, max_batch=1)
     try:
         state, so, sg, sw, got, want = None, None, None, None, [], []
         for i, ch in enumerate(padded):

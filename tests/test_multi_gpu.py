@@ -44,12 +44,14 @@ def test_world2_sessions_gather_matches_single_process(tmp_path):
 @pytest.mark.gpu
 def test_bench_world2_strong_scaling_rehearsal():
     r = _torchrun(["bench.py", "--gpus", "2", "--dist-backend", "gloo", "--global-batch", "64", "--steps", "4",
-                   "--warmup", "1", "--alt", "0", "--config4", "32", "--cpu-baseline-s", "0"], timeout=240)
+                   "--warmup", "1", "--alt", "0", "--config4", "32", "--config5", "32", "--cpu-baseline-s", "0"],
+                  timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["config"]["global_batch"] == 64
     assert out["config"]["batch_per_gpu"] == 32 and out["value"] > 0
-    c4 = out["alt_workloads"][0]
+    c4, c5 = out["alt_workloads"]
     assert c4["global_batch"] == 32 and c4["batch_per_gpu"] == 16 and c4["scaling"] == "strong"
+    assert c5["dtype"] == "fp8" and c5["batch_per_gpu"] == 16 and c5["value"] > 0
