@@ -72,13 +72,21 @@ int tone_session_set_weight(tone_session *s, const char *name, const float *host
  * (SwiGLU/GLU pairs interleaved, q|k|v concatenated) and upload the weights. */
 int tone_session_finalize(tone_session *s);
 
+/* Chunk length of the session's steps, before tone_session_finalize: 2400 samples (300 ms, default;
+ * tone/onnx_wrapper.py:32 AUDIO_CHUNK_SAMPLES) or 3200 (400 ms: the Triton ensemble's chunk,
+ * triton/ensemble/config.pbtxt:12-18; tone/scripts/export.py:139-157 chunk_duration_ms).  The flat state
+ * layout is the same; a 400 ms step reads signal [batch][3200] and writes logprobs [batch][13][35]. */
+int tone_session_set_chunk(tone_session *s, int chunk_samples);
+/* Acoustic frames per step: 10 (300 ms) or 13 (400 ms). */
+int tone_session_frames_per_chunk(const tone_session *s);
+
 /* Enable (1) / disable (0) hipGraph capture+replay of the per-step kernel sequence, keyed by
  * (batch, I/O pointers, frame_info pointer, state stride).  At most 16 executable graphs are kept
  * (least recently used evicted), so callers should reuse fixed I/O buffers.  Runs on the NULL stream,
  * with timing on, or with a debug stop set are never captured.  Default 0. */
 int tone_session_set_graph(tone_session *s, int enable);
 
-/* Optional per-frame decode outputs of later runs (device pointer, int32 [batch][10], or NULL):
+/* Optional per-frame decode outputs of later runs (device pointer, int32 [batch][frames], or NULL):
  *   frame_info = greedy CTC token (argmax over 35, first index on ties; tone/decoder.py:57)
  *              | speech flag << 8 (exp(lp[33]) + exp(lp[34]) <= 0.9; tone/logprob_splitter.py:134)
  * computed in the head kernel from the logprobs it writes.  Replaces the host-side argmax and
@@ -86,9 +94,9 @@ int tone_session_set_graph(tone_session *s, int enable);
 int tone_session_set_frame_info(tone_session *s, int32_t *frame_info);
 
 /* One streaming step for `batch` independent streams.
- *   signal      int32  [batch][2400]          PCM, int16 range (validated by the caller)
+ *   signal      int32  [batch][2400 | 3200]   PCM, int16 range (validated by the caller)
  *   state_in    fp16   [batch][state_stride]  first 219729 elements are the flat state
- *   logprobs    fp32   [batch][10][35]
+ *   logprobs    fp32   [batch][10 | 13][35]   (tone_session_frames_per_chunk)
  *   state_out   fp16   [batch][state_stride]  must not alias state_in
  * state_stride >= 219729 (elements). */
 int tone_session_run(tone_session *s, const int32_t *signal, const uint16_t *state_in, float *logprobs,

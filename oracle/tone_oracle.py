@@ -232,21 +232,23 @@ class ToneOracle:
         cat1 = np.concatenate([st.sub1[:, 0].astype(F32), x], axis=1)              # (B, 40, 64)
         nst["sub1"] = fp16(cat1[:, None, -C.SUB1_STATE:])
         kt, kf = C.SUB_K[0]
-        win = np.lib.stride_tricks.sliding_window_view(cat1, (kt, kf), axis=(1, 2))  # (B,30,44,11,21)
+        mt = x.shape[1]                                                              # 30 (300 ms) | 40 (400 ms)
+        win = np.lib.stride_tricks.sliding_window_view(cat1, (kt, kf), axis=(1, 2))  # (B,mt,44,11,21)
         w1 = W[pe + "conv.0.0.weight"].reshape(C.SUB_CH[0], -1)
-        y1 = win.reshape(b, 30, C.SUB1_F, -1) @ w1.T + W[pe + "conv.0.0.bias"]       # (B,30,44,32)
+        y1 = win.reshape(b, mt, C.SUB1_F, -1) @ w1.T + W[pe + "conv.0.0.bias"]       # (B,mt,44,32)
         y1 = silu(bn_eval(y1, W, pe + "conv.0.1.", axis=3))
         y1 = np.ascontiguousarray(y1.transpose(0, 3, 1, 2))                          # (B,32,30,44)
         cat2 = np.concatenate([st.sub2.astype(F32), y1], axis=2)                     # (B,32,38,44)
         nst["sub2"] = fp16(cat2[:, :, -C.SUB2_STATE:])
         kt, kf = C.SUB_K[1]
         win2 = np.lib.stride_tricks.sliding_window_view(cat2, (kt, kf), axis=(2, 3))[:, :, :: C.SUB_STRIDE[1][0]]
-        # win2: (B, 32, 10, 34, 11, 11) -> (B, 10, 34, 32*11*11)
-        a2 = np.ascontiguousarray(win2.transpose(0, 2, 3, 1, 4, 5)).reshape(b, 10, C.SUB2_F, -1)
+        # win2: (B, 32, T, 34, 11, 11) -> (B, T, 34, 32*11*11); T = 10 | 13 (a 400 ms chunk leaves row 47 unread)
+        t_out = win2.shape[2]
+        a2 = np.ascontiguousarray(win2.transpose(0, 2, 3, 1, 4, 5)).reshape(b, t_out, C.SUB2_F, -1)
         w2 = W[pe + "conv.1.0.weight"].reshape(C.SUB_CH[1], -1)
         y2 = a2 @ w2.T + W[pe + "conv.1.0.bias"]                                    # (B,10,34,64)
         y2 = silu(bn_eval(y2, W, pe + "conv.1.1.", axis=3))
-        flat = np.ascontiguousarray(y2.transpose(0, 1, 3, 2)).reshape(b, 10, C.SUB_OUT_IN)  # c*34+f
+        flat = np.ascontiguousarray(y2.transpose(0, 1, 3, 2)).reshape(b, t_out, C.SUB_OUT_IN)  # c*34+f
         x = linear(flat, W[pe + "out.weight"])
         return rmsnorm(x, W[pe + "out_norm.weight"])
 
@@ -385,8 +387,12 @@ class ToneOracle:
                 residual = x
                 x = self.reduce(x, st, nst)
             if L == C.UPSAMPLE_POS:
-                # TemporalUpsampling (conformer_blocks.py:955-988): repeat x2, pad, trim, +residual
-                up = np.repeat(x, C.REDUCTION_FACTOR, axis=1)[:, : residual.shape[1]]
+                # TemporalUpsampling (conformer_blocks.py:955-988): repeat x2, right-pad 1, trim to T,
+                # +residual (the pad frame is live for T = 13: 2 x 6 = 12 < 13)
+                rep = np.repeat(x, C.REDUCTION_FACTOR, axis=1)
+                up = np.zeros_like(residual)
+                n = min(rep.shape[1], residual.shape[1])
+                up[:, :n] = rep[:, :n]
                 x = up + residual
             if trace is not None:
                 trace.append(x)
@@ -394,11 +400,15 @@ class ToneOracle:
 
     def step(self, pcm: np.ndarray, state: np.ndarray | None = None, trace: list | None = None
              ) -> tuple[np.ndarray, np.ndarray]:
-        """pcm (B, 2400[,1]) int32, flat state (B, 219729) fp16 | None -> (logprobs fp32, state fp16).
+        """pcm (B, 2400 | 3200 [,1]) int32, flat state (B, 219729) fp16 | None -> (logprobs fp32, state fp16).
+        A 3200-sample (400 ms) chunk gives 13 frames; the state layout is the same.
 
         ``trace`` (optional list) receives the stage outputs the HIP path exposes for debugging:
         [feats (B,30,64), pre-encode output (B,10,384), layer 0 output, ..., layer 15 output]."""
-        pcm = np.asarray(pcm).reshape(pcm.shape[0], C.AUDIO_CHUNK_SAMPLES)
+        pcm = np.asarray(pcm)
+        pcm = pcm.reshape(pcm.shape[0], -1)
+        if pcm.shape[1] not in (2400, 3200):
+            raise ValueError(f"chunk of {pcm.shape[1]} samples (2400 or 3200)")
         b = pcm.shape[0]
         st = StreamState.zeros(b) if state is None else StreamState.unflatten(np.asarray(state, np.float16))
         nst: dict = {}
@@ -411,7 +421,7 @@ class ToneOracle:
             preproc=nst["preproc"],
             mhsa=np.stack(nst["mhsa"], axis=1),
             conv=np.stack(nst["conv"], axis=1),
-            mhsa_len=fp16(np.minimum(st.mhsa_len.astype(F32) + C.CHUNK_FRAMES, C.MHSA_STATE)),
+            mhsa_len=fp16(np.minimum(st.mhsa_len.astype(F32) + logp.shape[1], C.MHSA_STATE)),
             sub1=nst["sub1"],
             sub2=nst["sub2"],
             reduction=nst["reduction"],

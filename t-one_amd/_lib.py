@@ -23,6 +23,8 @@ SIGNATURES = {
     "tone_session_set_weight": (_c_int, [_c_void_p, _c_char_p, _c_void_p, _c_int64]),
     "tone_session_finalize": (_c_int, [_c_void_p]),
     "tone_session_set_graph": (_c_int, [_c_void_p, _c_int]),
+    "tone_session_set_chunk": (_c_int, [_c_void_p, _c_int]),
+    "tone_session_frames_per_chunk": (_c_int, [_c_void_p]),
     "tone_session_set_frame_info": (_c_int, [_c_void_p, _c_void_p]),
     "tone_session_run": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int64, _c_void_p]),
     "tone_session_run_slots": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int64, _c_void_p, _c_int, _c_void_p]),

@@ -8,7 +8,7 @@
 namespace tone {
 
 // ---- model constants (t-one_amd/config.py; tone/training/model_wrapper.py:27-115) -------------
-constexpr int kChunk = 2400;
+constexpr int kChunk = 2400;                  // 300 ms (the defaults below; 400 ms: Geom)
 constexpr int kPreState = 80;
 constexpr int kWave = kChunk + kPreState;     // 2480 samples per mel pass
 constexpr int kMelT = 30;                     // mel frames per chunk
@@ -36,6 +36,27 @@ constexpr int kConv2KPad = 3904;              // next multiple of 64 (bf16 K-ste
 constexpr int kMelPowCols = 128;              // 81 power bins padded to 4 x 32
 
 // flat state offsets (elements, per stream)
+// Chunk geometry.  The reference streams 300 ms (StreamingCTCModel.AUDIO_CHUNK_SAMPLES = 2400) and
+// exports / serves a 400 ms variant (tone/scripts/export.py:139-157 chunk_duration_ms;
+// triton/ensemble/config.pbtxt:12-18: 3200 samples).  The state layout is the same for both (its
+// sizes are fixed by the model, conformer.py:235-290); what changes per chunk is:
+//   wave   = chunk + 80 carried samples            2480 | 3280
+//   melT   = (wave - 160) / 80 + 1                  30   | 40    (feats.py:95-102)
+//   sub2In = 8 carried rows + melT                  38   | 48    (conformer_blocks.py:631-641)
+//   T      = (sub2In - 11) / 3 + 1                  10   | 13    (conv2 stride 3; 400 ms leaves row 47 unread)
+//   Tr     = (T + 1 - 3) / 2 + 1                    5    | 6     (CausalTemporalReduction, streaming branch)
+// and the upsampling pads one frame back to T (conformer_blocks.py:978-981: live for T = 13).
+struct Geom {
+  int chunk, wave, melT, sub2In, T, Tr;
+};
+__host__ __device__ constexpr Geom make_geom(int chunk) {
+  return Geom{chunk, chunk + 80, (chunk + 80 - 160) / 80 + 1, 8 + (chunk + 80 - 160) / 80 + 1,
+              (8 + (chunk + 80 - 160) / 80 + 1 - 11) / 3 + 1, ((8 + (chunk + 80 - 160) / 80 + 1 - 11) / 3 + 1 + 1 - 3) / 2 + 1};
+}
+constexpr int kChunkMax = 3200, kWaveMax = 3280, kMelTMax = 40, kSub2InMax = 48, kTMax = 13, kTrMax = 6;
+static_assert(make_geom(2400).T == 10 && make_geom(2400).Tr == 5 && make_geom(2400).melT == 30, "300 ms geometry");
+static_assert(make_geom(3200).T == 13 && make_geom(3200).Tr == 6 && make_geom(3200).melT == 40, "400 ms geometry");
+
 constexpr int64_t kOffPre = 0;
 constexpr int64_t kOffMhsa = 80;
 constexpr int64_t kOffConv = 23120;

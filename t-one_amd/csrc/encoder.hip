@@ -111,7 +111,6 @@ hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, i
 //   ctx = P . V: lane c < 48 owns output column c; its TK values of V are loaded straight into
 //   registers at kernel start (one coalesced row per load), P rows are read from LDS as
 //   broadcast float4s, the T output rows accumulate independently.
-constexpr int kMaxT = 10, kMaxTK = 40;
 
 template <int T, int S, bool REC, bool OBF>
 __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
@@ -235,15 +234,22 @@ __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
 template <bool OBF>
 static hipError_t launch_attention_t(const AttnArgs& a, hipStream_t st) {
   const dim3 grid(a.B * 2), block(256);
+  // (T, S) of the 300 ms chunk: (10 | 5, 0), layer 14 (5, 15), layer 15 (10, 30); 400 ms: T 13 | 6
   if (!a.recompute) {
     if (a.S != 0) return hipErrorInvalidValue;
     if (a.T == 10) hipLaunchKernelGGL((attention_kernel<10, 0, false, OBF>), grid, block, 0, st, a);
     else if (a.T == 5) hipLaunchKernelGGL((attention_kernel<5, 0, false, OBF>), grid, block, 0, st, a);
+    else if (a.T == 13) hipLaunchKernelGGL((attention_kernel<13, 0, false, OBF>), grid, block, 0, st, a);
+    else if (a.T == 6) hipLaunchKernelGGL((attention_kernel<6, 0, false, OBF>), grid, block, 0, st, a);
     else return hipErrorInvalidValue;
   } else if (a.T == 10 && a.S == 0) hipLaunchKernelGGL((attention_kernel<10, 0, true, OBF>), grid, block, 0, st, a);
   else if (a.T == 5 && a.S == 0) hipLaunchKernelGGL((attention_kernel<5, 0, true, OBF>), grid, block, 0, st, a);
   else if (a.T == 5 && a.S == 15) hipLaunchKernelGGL((attention_kernel<5, 15, true, OBF>), grid, block, 0, st, a);
   else if (a.T == 10 && a.S == 30) hipLaunchKernelGGL((attention_kernel<10, 30, true, OBF>), grid, block, 0, st, a);
+  else if (a.T == 13 && a.S == 0) hipLaunchKernelGGL((attention_kernel<13, 0, true, OBF>), grid, block, 0, st, a);
+  else if (a.T == 6 && a.S == 0) hipLaunchKernelGGL((attention_kernel<6, 0, true, OBF>), grid, block, 0, st, a);
+  else if (a.T == 6 && a.S == 15) hipLaunchKernelGGL((attention_kernel<6, 15, true, OBF>), grid, block, 0, st, a);
+  else if (a.T == 13 && a.S == 30) hipLaunchKernelGGL((attention_kernel<13, 30, true, OBF>), grid, block, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -367,56 +373,69 @@ hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, 
                           : launch_dwconv_t<kT, false>(g, s, layer, w, b, out, B, st);
   if (T == kT / 2) return obf ? launch_dwconv_t<kT / 2, true>(g, s, layer, w, b, out, B, st)
                               : launch_dwconv_t<kT / 2, false>(g, s, layer, w, b, out, B, st);
+  if (T == 13) return obf ? launch_dwconv_t<13, true>(g, s, layer, w, b, out, B, st)     // 400 ms chunks
+                          : launch_dwconv_t<13, false>(g, s, layer, w, b, out, B, st);
+  if (T == 6) return obf ? launch_dwconv_t<6, true>(g, s, layer, w, b, out, B, st)
+                         : launch_dwconv_t<6, false>(g, s, layer, w, b, out, B, st);
   return hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------------------------
 // CausalTemporalReduction.forward streaming branch (conformer_blocks.py:888-907), grouped part:
-//   x = [state (1) ; x^T (10)] per channel; next state = x[:, -1:]
-//   y[o][t] = bias[o] + sum_{k<3} w[o][k] x[o/4][2t+k], o < 1536, t < 5
-template <bool OBF>
+//   x = [state (1) ; x^T (T)] per channel; next state = x[:, -1:]
+//   y[o][t] = bias[o] + sum_{k<3} w[o][k] x[o/4][2t+k], o < 1536, t < Tr = (T + 1 - 3) / 2 + 1
+//   (no padding in the streaming branch: T = 13 gives Tr = 6 and leaves the last frame to the state)
+template <bool OBF, int T>
 __global__ void __launch_bounds__(256) reduce_conv_kernel(const float* __restrict__ x, StateRef s,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           void* __restrict__ y, int B) {
+  constexpr int TR = (T + 1 - 3) / 2 + 1;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= B * kD) return;
   const int b = idx / kD, c = idx % kD;
-  float xc[kT + 1];
+  float xc[T + 1];
   xc[0] = __half2float(s.in[s.row_in(b) + kOffRed + c]);
-  for (int t = 0; t < kT; ++t) xc[t + 1] = x[((int64_t)b * kT + t) * kD + c];
-  s.out[s.row_out(b) + kOffRed + c] = __float2half_rn(xc[kT]);
+  for (int t = 0; t < T; ++t) xc[t + 1] = x[((int64_t)b * T + t) * kD + c];
+  s.out[s.row_out(b) + kOffRed + c] = __float2half_rn(xc[T]);
   for (int q = 0; q < 4; ++q) {
     const int o = 4 * c + q;
     const float w0 = w[o * 3], w1 = w[o * 3 + 1], w2 = w[o * 3 + 2], bo = bias[o];
-    for (int t = 0; t < kT / 2; ++t)
-      store_act<OBF>(y, ((int64_t)b * (kT / 2) + t) * (4 * kD) + o, bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2]);
+    for (int t = 0; t < TR; ++t)
+      store_act<OBF>(y, ((int64_t)b * TR + t) * (4 * kD) + o, bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2]);
   }
 }
 
 hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
-                              hipStream_t st) {
-  if (obf) hipLaunchKernelGGL(reduce_conv_kernel<true>, dim3((B * kD + 255) / 256), dim3(256), 0, st, x, s, w, b, y, B);
-  else hipLaunchKernelGGL(reduce_conv_kernel<false>, dim3((B * kD + 255) / 256), dim3(256), 0, st, x, s, w, b, y, B);
+                              int T, hipStream_t st) {
+  const dim3 grid((B * kD + 255) / 256), block(256);
+  if (T == kT && obf) hipLaunchKernelGGL((reduce_conv_kernel<true, kT>), grid, block, 0, st, x, s, w, b, y, B);
+  else if (T == kT) hipLaunchKernelGGL((reduce_conv_kernel<false, kT>), grid, block, 0, st, x, s, w, b, y, B);
+  else if (T == 13 && obf) hipLaunchKernelGGL((reduce_conv_kernel<true, 13>), grid, block, 0, st, x, s, w, b, y, B);
+  else if (T == 13) hipLaunchKernelGGL((reduce_conv_kernel<false, 13>), grid, block, 0, st, x, s, w, b, y, B);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
-// TemporalUpsampling (conformer_blocks.py:955-988): repeat_interleave x2, trim to 10, + residual.
+// TemporalUpsampling (conformer_blocks.py:955-988): repeat_interleave x2, right-pad 1, trim to T, + residual.
+// Frames t < 2 Tr take x5[t / 2]; a frame past 2 Tr (t = 12 of a 400 ms chunk: 2 x 6 < 13) is the zero pad,
+// so it keeps the residual alone.
 __global__ void __launch_bounds__(256) upsample_add_kernel(float* __restrict__ x10, const float* __restrict__ x5, int B,
-                                                           uint16_t* __restrict__ shadow, int64_t plane) {
+                                                           int T, int Tr, uint16_t* __restrict__ shadow, int64_t plane) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (int64_t)B * kT * kD) return;
+  if (idx >= (int64_t)B * T * kD) return;
   const int64_t row = idx / kD;
   const int c = idx % kD;
-  const int64_t b = row / kT, t = row % kT;
-  const float v = x5[(b * (kT / 2) + t / 2) * kD + c] + x10[idx];
+  const int64_t b = row / T, t = row % T;
+  const float v = (t < 2 * Tr ? x5[(b * Tr + t / 2) * kD + c] : 0.0f) + x10[idx];
   x10[idx] = v;
   if (shadow) store_shadow(shadow, plane, idx, v);
 }
 
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, int64_t plane, hipStream_t st) {
-  const int64_t n = (int64_t)B * kT * kD;
-  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, shadow,
+hipError_t launch_upsample_add(float* x10, const float* x5, int B, int T, uint16_t* shadow, int64_t plane, hipStream_t st) {
+  const int64_t n = (int64_t)B * T * kD;
+  const int Tr = (T + 1 - 3) / 2 + 1;
+  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr, shadow,
                      plane);
   return hipGetLastError();
 }

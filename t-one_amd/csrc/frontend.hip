@@ -19,25 +19,27 @@ __device__ __forceinline__ void barrier_lds_c2() {   // keeps LDS-DMA in flight 
 // x is stored as fp32 values for the spectrum GEMM (mel_gemms, gemm.hip).  Also writes
 // mhsa_len' = min(mhsa_len + 10, 30) (EncoderState.next, conformer_blocks.py:191).
 __global__ void __launch_bounds__(256) mel_prep_kernel(const int32_t* __restrict__ pcm, StateRef s,
-                                                       float* __restrict__ wave, int B) {
+                                                       float* __restrict__ wave, int B, int chunk, int T) {
+  const int wv = chunk + kPreState;
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (int64_t)B * kWave) return;
-  const int b = (int)(idx / kWave), i = (int)(idx % kWave);
+  if (idx >= (int64_t)B * wv) return;
+  const int b = (int)(idx / wv), i = (int)(idx % wv);
   const int64_t srow = s.row_in(b), orow = s.row_out(b);
   __half hv;
   if (i < kPreState) hv = s.in[srow + kOffPre + i];
-  else hv = __float2half_rn((float)pcm[(int64_t)b * kChunk + (i - kPreState)] / 32767.0f);
+  else hv = __float2half_rn((float)pcm[(int64_t)b * chunk + (i - kPreState)] / 32767.0f);
   wave[idx] = __half2float(hv);
-  if (i >= kChunk) s.out[orow + kOffPre + (i - kChunk)] = hv;
-  if (i == 0) {
+  if (i >= chunk) s.out[orow + kOffPre + (i - chunk)] = hv;
+  if (i == 0) {   // mhsa_len + T: EncoderState.state_keep_size = the chunk's frame count (conformer_blocks.py:206)
     const float ml = __half2float(s.in[srow + kOffMhsaLen]);
-    s.out[orow + kOffMhsaLen] = __float2half_rn(fminf(ml + (float)kT, (float)kMhsaS));
+    s.out[orow + kOffMhsaLen] = __float2half_rn(fminf(ml + (float)T, (float)kMhsaS));
   }
 }
 
-hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, hipStream_t st) {
-  const int64_t n = (int64_t)B * kWave;
-  hipLaunchKernelGGL(mel_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pcm, s, wave, B);
+hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, int chunk, hipStream_t st) {
+  const Geom g = make_geom(chunk);
+  const int64_t n = (int64_t)B * g.wave;
+  hipLaunchKernelGGL(mel_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pcm, s, wave, B, chunk, g.T);
   return hipGetLastError();
 }
 
@@ -52,17 +54,18 @@ hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, h
 // from x1 in LDS.
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-constexpr int kPos1 = kMelT * kSub1F;       // 1320
 
 // ---- fp32 (exact-fp32 MFMA v_mfma_f32_32x32x2_f32): 8 waves per stream, 32-position tiles; the tap
 // loop runs kt (11) x kf pairs (11, the 22nd tap zero-weighted), so the gathered x1 address is plain
 // arithmetic (no tap table).
 constexpr int kKfP = 22;                    // kf padded to an even count (fp32 path)
 
+template <int MT>   // mel frames per chunk: 30 (300 ms) | 40 (400 ms)
 __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__ feats, StateRef s,
                                                        const float* __restrict__ pre_norm_w,
                                                        const float* __restrict__ w1, const float* __restrict__ scale1,
                                                        const float* __restrict__ shift1, float* __restrict__ x2) {
+  constexpr int kMelT = MT, kSub2In = kSub2S + MT, kPos1 = MT * kSub1F;   // 1320 positions at 300 ms
   __shared__ float x1[(kSub1S + kMelT) * kMels + 32];   // +32: taps past column 63 read zeros
   __shared__ float wk[kSub1C][kSub1Kt * kKfP + 1];
   __shared__ float sc[kSub1C], sh[kSub1C];
@@ -145,13 +148,15 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
 // channels (2 MFMA column tiles); 90 tiles per stream over 8 waves.
 constexpr int kX1Cols = 80;                 // shifted-copy row length (taps reach column 43 + 31)
 
+template <int MT>
 __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict__ feats, StateRef s,
                                                         const float* __restrict__ pre_norm_w,
                                                         const uint16_t* __restrict__ w1t, const float* __restrict__ scale1,
                                                         const float* __restrict__ shift1, uint16_t* __restrict__ x2) {
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
   typedef float f32x4 __attribute__((ext_vector_type(4)));
-  constexpr int kRows = kSub1S + kMelT;     // 40
+  constexpr int kMelT = MT, kSub2In = kSub2S + MT;
+  constexpr int kRows = kSub1S + kMelT;     // 40 (300 ms) | 50 (400 ms)
   // 8 shifted copies, each padded by 32 B so the copies start 8 banks apart (a wave's A reads hit
   // all 8 copies at the same in-copy offset)
   constexpr int kCopy = kRows * kX1Cols + 16;
@@ -243,17 +248,27 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
   }
 }
 
-hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
-                       const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st) {
+template <int MT>
+static hipError_t launch_sub1_t(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
+                                const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st) {
   if (x2_bf16) {
     if (!w1t) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sub1_bf16_kernel, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w,
+    hipLaunchKernelGGL(sub1_bf16_kernel<MT>, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w,
                        static_cast<const uint16_t*>(w1t), scale1, shift1, static_cast<uint16_t*>(x2));
   } else {
-    hipLaunchKernelGGL(sub1_f32_kernel, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w, w1, scale1, shift1,
+    hipLaunchKernelGGL(sub1_f32_kernel<MT>, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w, w1, scale1, shift1,
                        static_cast<float*>(x2));
   }
   return hipGetLastError();
+}
+
+hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
+                       const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, int chunk,
+                       hipStream_t st) {
+  const int mt = make_geom(chunk).melT;
+  if (mt == 30) return launch_sub1_t<30>(feats, s, pre_norm_w, w1, w1t, scale1, shift1, x2, x2_bf16, B, st);
+  if (mt == 40) return launch_sub1_t<40>(feats, s, pre_norm_w, w1, w1t, scale1, shift1, x2, x2_bf16, B, st);
+  return hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -422,19 +437,26 @@ constexpr int kC3Pos = kC3Rows * kSub2F;                          // 170
 constexpr int kC3Tiles = (kC3Pos + 15) / 16;                      // 11
 static_assert(kC3Slab * 4 + 2 * kC3Tap * 4 + 2 * kSub2C * 4 <= 160 * 1024, "conv2_x3 LDS");
 
-template <int NWV>   // waves per workgroup (8: two per SIMD; 4: one per SIMD, 3 tiles each)
+// 400 ms (T = 13): three workgroups per stream (5 + 5 + 3 output rows); the last one's slab window
+// is clamped to the stream's 48 input rows and its positions past row 13 are not stored.
+template <int NWV, int T>   // waves per workgroup (8: two per SIMD; 4: one per SIMD, 3 tiles each); frames
 __global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2x,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        float* __restrict__ flat) {
+  constexpr int kParts = (T + kC3Rows - 1) / kC3Rows;
+  constexpr int kIn = (T == make_geom(3200).T ? make_geom(3200) : make_geom(2400)).sub2In;   // input rows per stream
+  constexpr int kC2PosT = T * kSub2F;
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float lds[kC3Slab + 2 * kC3Tap + 2 * kSub2C];   // slab | ring | sc | sh
   float* ring = lds + kC3Slab;
   float* sc = ring + 2 * kC3Tap;
   float* sh = sc + kSub2C;
-  const int b = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int b = blockIdx.x / kParts, half = blockIdx.x % kParts;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const float* xb = x2 + ((int64_t)b * kSub2In * kSub1F + half * kSub2Stride * kC3Rows * kSub1F) * kSub1C;
+  const int rows = min(kC3Rows, T - half * kC3Rows), posT = rows * kSub2F;   // this part's output rows
+  const int in_left = (kIn - half * kSub2Stride * kC3Rows) * kSub1F;          // input positions left in the stream
+  const float* xb = x2 + ((int64_t)b * kIn * kSub1F + half * kSub2Stride * kC3Rows * kSub1F) * kSub1C;
   if (tid < kSub2C) {
     sc[tid] = scale[tid];
     sh[tid] = shift[tid];
@@ -453,7 +475,7 @@ __global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restr
   };
   for (int pc = wid; pc < kC3SlabPieces; pc += NWV) {     // the slab, once: lane -> (q, swizzled slot)
     const int L = pc * 64 + lane, q = L >> 3, s = (L & 7) ^ ((q >> 1) & 7);
-    const float* src = xb + min(q, kC3In - 1) * kSub1C + s * 4;
+    const float* src = xb + min(q, min(kC3In, in_left) - 1) * kSub1C + s * 4;
 #if defined(__HIP_DEVICE_COMPILE__)
     __builtin_amdgcn_global_load_lds(src, lds + pc * 256, 16, 0, 0);
 #else
@@ -532,8 +554,8 @@ __global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restr
   for (int k = 0; k < KT; ++k) {
     if (k >= ntile) break;
     const int p = (wid + NWV * k) * 16 + n;
-    if (p >= kC3Pos) continue;
-    float* dst = flat + ((int64_t)b * kC2Pos + half * kC3Pos + p) * kSub2C;
+    if (p >= posT) continue;
+    float* dst = flat + ((int64_t)b * kC2PosT + half * kC3Pos + p) * kSub2C;
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       const int ch = 16 * ct + 4 * g;
@@ -548,17 +570,18 @@ __global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restr
 }
 
 hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, const float* shift, void* flat, int B,
-                           hipStream_t st) {
+                           int T, hipStream_t st) {
   static const int nwv = [] {   // TONE_CONV2_WAVES (sweeps only): 8 (default) or 4
     const char* e = std::getenv("TONE_CONV2_WAVES");
     return e ? std::atoi(e) : 8;
   }();
-  if (nwv == 4)
-    hipLaunchKernelGGL(conv2_x3_kernel<4>, dim3(2 * B), dim3(256), 0, st, static_cast<const float*>(x2),
-                       static_cast<const uint16_t*>(w2x), scale, shift, static_cast<float*>(flat));
-  else
-    hipLaunchKernelGGL(conv2_x3_kernel<8>, dim3(2 * B), dim3(512), 0, st, static_cast<const float*>(x2),
-                       static_cast<const uint16_t*>(w2x), scale, shift, static_cast<float*>(flat));
+  const float* xs = static_cast<const float*>(x2);
+  const uint16_t* ws = static_cast<const uint16_t*>(w2x);
+  float* fl = static_cast<float*>(flat);
+  if (T == 13) hipLaunchKernelGGL((conv2_x3_kernel<8, 13>), dim3(3 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
+  else if (T != kT) return hipErrorInvalidValue;
+  else if (nwv == 4) hipLaunchKernelGGL((conv2_x3_kernel<4, kT>), dim3(2 * B), dim3(256), 0, st, xs, ws, scale, shift, fl);
+  else hipLaunchKernelGGL((conv2_x3_kernel<8, kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
   return hipGetLastError();
 }
 

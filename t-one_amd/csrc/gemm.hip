@@ -119,9 +119,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[T
 #pragma unroll
         for (int j = 0; j < TN; ++j) dst[cbase + j * 32] = acc[i][j][r];
       } else if constexpr (CONV2) {
-        const int b = row / (kT * kSub2F), rem = row % (kT * kSub2F);
-        const int t = rem / kSub2F, f = rem % kSub2F;
-        const int64_t o = ((int64_t)b * kT + t) * kSubOut + f * kSub2C;
+        const int64_t o = (int64_t)row * kSub2C;   // flat [B*T][34*64]: row (b, t, f) -> ((b T + t) 34 + f) 64
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int c = cbase + j * 32;
@@ -323,10 +321,10 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
     const int r = (tid + i * NT) / A_RV;
     const int gm = min(m0 + r, p.M - 1);
     rvalid[i] = (m0 + r) < p.M;
-    if constexpr (CONV2) {
-      const int b = gm / (kT * kSub2F), rem = gm % (kT * kSub2F);
+    if constexpr (CONV2) {   // chunk geometry from the launcher (conv_t frames, conv_in input rows)
+      const int b = gm / (p.conv_t * kSub2F), rem = gm % (p.conv_t * kSub2F);
       const int t = rem / kSub2F, f = rem % kSub2F;
-      rowoff[i] = (((int64_t)b * kSub2In + kSub2Stride * t) * kSub1F + f) * kSub1C;
+      rowoff[i] = (((int64_t)b * p.conv_in + kSub2Stride * t) * kSub1F + f) * kSub1C;
     } else {
       rowoff[i] = p.rpg ? (int64_t)(gm / p.rpg) * p.gstride + (int64_t)(gm % p.rpg) * p.lda : (int64_t)gm * p.lda;
     }
@@ -539,9 +537,9 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
     const int gm = min(m0 + row, p.M - 1);
     aslot[i] = lslot ^ (row & 7);
     if constexpr (CONV2) {
-      const int b = gm / (kT * kSub2F), rem = gm % (kT * kSub2F);
+      const int b = gm / (p.conv_t * kSub2F), rem = gm % (p.conv_t * kSub2F);
       const int t = rem / kSub2F, f = rem % kSub2F;
-      aoff[i] = (((int64_t)b * kSub2In + kSub2Stride * t) * kSub1F + f) * kSub1C;
+      aoff[i] = (((int64_t)b * p.conv_in + kSub2Stride * t) * kSub1F + f) * kSub1C;
     } else {
       aoff[i] = (p.rpg ? (int64_t)(gm / p.rpg) * p.gstride + (int64_t)(gm % p.rpg) * p.lda : (int64_t)gm * p.lda) +
                 aslot[i] * 8;
@@ -1103,18 +1101,22 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
 }
 
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st, const void* w2x) {
-  if (bf16) return launch_conv2_bf16(x2, w, scale, shift, flat, B, st);   // per-stream LDS slab (frontend.hip)
-  if (w2x) return launch_conv2_x3(x2, w2x, scale, shift, flat, B, st);    // fp32 split mode (frontend.hip)
+                      bool bf16, hipStream_t st, const void* w2x, int chunk) {
+  const Geom geo = make_geom(chunk);
+  // per-stream LDS slab kernel (frontend.hip): the 300 ms slab (38 rows, 107 KB) fits, 400 ms (48) does not
+  if (bf16 && geo.T == kT) return launch_conv2_bf16(x2, w, scale, shift, flat, B, st);
+  if (w2x) return launch_conv2_x3(x2, w2x, scale, shift, flat, B, geo.T, st);    // fp32 split mode (frontend.hip)
   GemmArgs a{};
   a.A = x2;
   a.W = w;
   a.C = flat;
   a.bias = shift;
   a.scale = scale;
-  a.M = B * kT * kSub2F;
+  a.M = B * geo.T * kSub2F;
   a.N = kSub2C;
   a.K = bf16 ? kConv2KPad : kSub2Kt * kSub2Kf * kSub1C;
+  a.conv_t = geo.T;
+  a.conv_in = geo.sub2In;
   const dim3 grid((a.M + 127) / 128), block(256);
   if (bf16) hipLaunchKernelGGL((gemm_glds_kernel<Tile<128, 64, 4, 1>, EPI_CONV2, true, 2>), grid, block, 0, st, a);
   else hipLaunchKernelGGL((gemm_kernel<Tile<128, 64, 4, 1>, EPI_CONV2, false, false, false, false>), grid, block, 0, st, a);
@@ -1125,16 +1127,17 @@ hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const f
 //   power[(b,t)][f] = |sum_k basis_f[k] wave[b][80t + k]|^2      K = 160, N = 256 (re/im blocks)
 //   feats[(b,t)][m] = fp16(log(sum_f fbank[m][f] power[f] + 2^-24))  K = 128, N = 128 (64 used)
 hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank_p, float* power, float* feats, int B,
-                     hipStream_t st) {
+                     int chunk, hipStream_t st) {
+  const Geom geo = make_geom(chunk);
   GemmArgs a{};
   a.A = wave;
   a.lda = kHop;
-  a.rpg = kMelT;
-  a.gstride = kWave;
+  a.rpg = geo.melT;
+  a.gstride = geo.wave;
   a.W = basis_p;
   a.C = power;
   a.ldc = kMelPowCols;
-  a.M = B * kMelT;
+  a.M = B * geo.melT;
   a.N = 2 * kMelPowCols;
   a.K = kWin;
   const dim3 block(256);
@@ -1149,7 +1152,7 @@ hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank
   m.C = feats;
   m.ldc = kMels;
   m.n_out = kMels;
-  m.M = B * kMelT;
+  m.M = B * geo.melT;
   m.N = 128;
   m.K = kMelPowCols;
   hipLaunchKernelGGL((gemm_kernel<Tile<64, 128, 2, 2>, EPI_LOGMEL, false, false, false, false>),

@@ -44,6 +44,7 @@ struct GemmArgs {
   int64_t a_plane;    // A given as 3 bf16 planes (lda in elements) instead of fp32
   int64_t c_plane;    // STORE / SWIGLU / GLU: C written as 3 bf16 planes instead of fp32
   int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
+  int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -92,7 +93,7 @@ hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, h
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,
 // epilogue SiLU(acc*scale + shift) -> flat [B*10][34*64] (f-major, channel-minor).
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st, const void* w2x = nullptr);
+                      bool bf16, hipStream_t st, const void* w2x = nullptr, int chunk = kChunk);
 
 // a3 conv2 in bf16 mode, one workgroup per stream over an LDS-resident input slab (frontend.hip);
 // x2 bf16 [B][38][44][32], w2c bf16 [64][3904] tap-major, flat bf16 [B*10][34*64]
@@ -101,24 +102,25 @@ hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale
 // a3 conv2 in fp32 (split) mode: two workgroups per stream over fp32 LDS slabs, exact 3-way bf16
 // splits on the bf16 MFMA (frontend.hip); x2 fp32 [B][38][44][32], flat fp32 [B*10][34*64]
 hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, const float* shift, void* flat, int B,
-                           hipStream_t st);
+                           int T, hipStream_t st);
 // host: pack the split planes [3][64][121][32] (bf16 bits) into the conv2_x3 tap-major layout
 void conv2_x3_pack(const uint16_t* planes, uint16_t* w2x);
 
 // a2 log-mel on the fp32 MFMA: power spectrum GEMM over overlapping windows, then filterbank GEMM
 // with the log / fp16 epilogue.  wave [B][2480] fp32 (from launch_mel_prep).
 hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank_p, float* power, float* feats, int B,
-                     hipStream_t st);
+                     int chunk, hipStream_t st);
 
 // a1: PCM -> fp16 wave [B][2480] (fp32 storage) with the 80 carried samples; next preproc state
 // and mhsa_len of the next state.
-hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, hipStream_t st);
+hipError_t launch_mel_prep(const int32_t* pcm, StateRef s, float* wave, int B, int chunk, hipStream_t st);
 
 // a3 part 1: pre-norm RMSNorm(64) + sub1 state + Conv2d(1->32,k11x21) + BN + SiLU, written with the
 // carried sub2 rows as the channels-last conv2 input x2 [B][38][44][32]; next sub1/sub2 states.
 // w1: fp32 [32][11][21] (fp32 mode); w1t: bf16 [11][32][32] kf-padded (bf16 mode)
 hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, const float* w1, const void* w1t,
-                       const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, hipStream_t st);
+                       const float* scale1, const float* shift1, void* x2, bool x2_bf16, int B, int chunk,
+                       hipStream_t st);
 
 // In-place RMSNorm over rows of 384 (norm_out, out_norm); optional bf16 shadow of the result
 // (3 split planes `plane` elements apart when plane > 0).
@@ -152,10 +154,10 @@ hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, 
 
 // a11: reduction state + grouped conv (384->1536, k3, s2) -> y [B*5][1536]
 hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
-                              hipStream_t st);
+                              int T, hipStream_t st);
 
 // a12: x10[b*10+t] += x5[b*5+t/2]
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, uint16_t* shadow, int64_t plane, hipStream_t st);
+hipError_t launch_upsample_add(float* x10, const float* x5, int B, int T, uint16_t* shadow, int64_t plane, hipStream_t st);
 
 // a14: logits = x . Wd^T + bd, log_softmax over 35 classes -> logprobs [B*10][35]
 // a14 + decode flags: logprobs [rows][35]; optional frame_info[row] = greedy token | speech flag << 8

@@ -77,6 +77,7 @@ struct LayerW {
 struct tone_session {
   int device = 0;
   int precision = TONE_PRECISION_FP32;
+  Geom geo = make_geom(kChunk);   // chunk geometry (tone_session_set_chunk; 300 ms by default)
   int max_batch = 0;
   bool finalized = false;
   bool use_graph = false;
@@ -323,14 +324,15 @@ std::vector<float> make_fbank() {
   return fb;
 }
 
-// RotaryPositionalEmbeddings._build_state (submodules.py:120-140), positions -30..9, 16 freqs.
+// RotaryPositionalEmbeddings._build_state (submodules.py:120-140), positions -30..12 (cached keys of
+// layer 15 through the last frame of a 400 ms chunk), 16 freqs.
 void make_rope(std::vector<float>& cs, std::vector<float>& sn) {
-  cs.resize(40 * 16);
-  sn.resize(40 * 16);
+  cs.resize((30 + kTMax) * 16);
+  sn.resize((30 + kTMax) * 16);
   for (int j = 0; j < 16; ++j) {
     const float e = (float)(2 * j) / 32.0f;
     const float inv = 1.0f / std::pow(10000.0f, e);
-    for (int p = -30; p < 10; ++p) {
+    for (int p = -30; p < kTMax; ++p) {
       const float ang = (float)p * inv;
       cs[(p + 30) * 16 + j] = std::cos(ang);
       sn[(p + 30) * 16 + j] = std::sin(ang);
@@ -452,18 +454,20 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   const bool bf = bfmode(s), f8 = s->precision == TONE_PRECISION_FP8;
   uint16_t* shA = bf ? s->xbA : nullptr;
   uint16_t* shB = bf ? s->xbB : nullptr;
-  LAUNCH("mel_prep", launch_mel_prep(signal, sr, s->wave, B, st));
-  LAUNCH("mel", mel_gemms(s->wave, s->basis_p, s->fbank_p, s->power, s->feats, B, st));
+  const Geom& geo = s->geo;
+  LAUNCH("mel_prep", launch_mel_prep(signal, sr, s->wave, B, geo.chunk, st));
+  LAUNCH("mel", mel_gemms(s->wave, s->basis_p, s->fbank_p, s->power, s->feats, B, geo.chunk, st));
   if (s->debug_stop == 0) return TONE_OK;
-  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B, st));
-  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, s->w2x));
-  CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * kT, D, kSubOut,
+  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B, geo.chunk,
+                             st));
+  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, s->w2x, geo.chunk));
+  CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * geo.T, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
-  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * kT, shA, 0, st));
+  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st));
   if (s->debug_stop == 1) return TONE_OK;
   float* x = s->rA;
   uint16_t* xs = shA;           // bf16 shadow of x (bf16 mode)
-  int T = kT;
+  int T = geo.T;
   for (int l = 0; l < 16; ++l) {
     const LayerW& w = s->L[l];
     const int M = B * T;
@@ -556,22 +560,22 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     CALL(ffn(1));
     LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
-      LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, st));
-      CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * (kT / 2), D, 4 * D,
+      LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, geo.T, st));
+      CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * geo.Tr, D, 4 * D,
                      EPI_STORE, 0, nullptr, 1.0f, true, false, shB));
       x = s->rB;
       xs = shB;
-      T = kT / 2;
+      T = geo.Tr;
     }
     if (l == 14) {  // TemporalUpsampling (conformer.py:224-225)
-      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, shA, 0, st));
+      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, geo.T, shA, 0, st));
       x = s->rA;
       xs = shA;
-      T = kT;
+      T = geo.T;
     }
     if (s->debug_stop == 2 + l) return TONE_OK;
   }
-  LAUNCH("head", launch_head(s->rA, s->whead, s->bhead, logp, s->frame_info, B * kT, st));
+  LAUNCH("head", launch_head(s->rA, s->whead, s->bhead, logp, s->frame_info, B * geo.T, st));
   return TONE_OK;
 }
 
@@ -822,31 +826,31 @@ int finalize_weights(tone_session* s) {
 
   // activations
   const size_t MB = (size_t)s->max_batch;
-  CALL(dalloc(s, &s->wave, MB * kWave));
-  CALL(dalloc(s, &s->power, MB * kMelT * kMelPowCols));
-  CALL(dalloc(s, &s->feats, MB * kMelT * kMels));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->x2), MB * kSub2In * kSub1F * kSub1C));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->flat), MB * kT * kSubOut));
-  CALL(dalloc(s, &s->rA, MB * kT * D));
-  CALL(dalloc(s, &s->rB, MB * (kT / 2) * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->h), MB * kT * kDff));
-  CALL(dalloc(s, &s->qkv, MB * kT * 3 * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->xn), MB * kT * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->kv), MB * 40 * D));
-  CALL(dalloc(s, &s->kvp, MB * 40 * 2 * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->ctx), MB * kT * D));
-  CALL(dalloc(s, &s->g, MB * kT * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->d), MB * kT * D));
-  CALL(dalloc(s, &s->probs, MB * kHeads * kT * 40));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->yred), MB * (kT / 2) * 4 * D));
-  CALL(dalloc(s, &s->xbA, MB * kT * D));
-  CALL(dalloc(s, &s->xbB, MB * (kT / 2) * D));
+  CALL(dalloc(s, &s->wave, MB * kWaveMax));
+  CALL(dalloc(s, &s->power, MB * kMelTMax * kMelPowCols));
+  CALL(dalloc(s, &s->feats, MB * kMelTMax * kMels));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->x2), MB * kSub2InMax * kSub1F * kSub1C));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->flat), MB * kTMax * kSubOut));
+  CALL(dalloc(s, &s->rA, MB * kTMax * D));
+  CALL(dalloc(s, &s->rB, MB * kTrMax * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->h), MB * kTMax * kDff));
+  CALL(dalloc(s, &s->qkv, MB * kTMax * 3 * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->xn), MB * kTMax * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->kv), MB * (30 + kTMax) * D));
+  CALL(dalloc(s, &s->kvp, MB * (30 + kTMax) * 2 * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->ctx), MB * kTMax * D));
+  CALL(dalloc(s, &s->g, MB * kTMax * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->d), MB * kTMax * D));
+  CALL(dalloc(s, &s->probs, MB * kHeads * kTMax * (30 + kTMax)));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->yred), MB * kTrMax * 4 * D));
+  CALL(dalloc(s, &s->xbA, MB * kTMax * D));
+  CALL(dalloc(s, &s->xbB, MB * kTrMax * D));
   if (s->precision == TONE_PRECISION_FP8) {
-    CALL(dalloc(s, &s->a8, MB * 40 * D));            // the largest quantized input: layer 15's k/v rows
-    CALL(dalloc(s, &s->a8s, MB * 40 * (D / 32)));
-    CALL(dalloc(s, &s->inv8, MB * 40));
-    CALL(dalloc(s, &s->h8, MB * kT * kDff));
-    CALL(dalloc(s, &s->h8s, MB * kT * (kDff / 32)));
+    CALL(dalloc(s, &s->a8, MB * (30 + kTMax) * D));            // the largest quantized input: layer 15's k/v rows
+    CALL(dalloc(s, &s->a8s, MB * (30 + kTMax) * (D / 32)));
+    CALL(dalloc(s, &s->inv8, MB * (30 + kTMax)));
+    CALL(dalloc(s, &s->h8, MB * kTMax * kDff));
+    CALL(dalloc(s, &s->h8s, MB * kTMax * (kDff / 32)));
   }
   // split-K workspace: only small batches split (large ones fill the chip with whole-K tiles)
   s->ws_cap = 16ll << 20;
@@ -976,6 +980,17 @@ int tone_session_finalize(tone_session* s) {
   return TONE_OK;
 }
 
+int tone_session_set_chunk(tone_session* s, int chunk_samples) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  if (s->finalized) return fail(TONE_E_STATE, "tone_session_set_chunk must precede tone_session_finalize");
+  if (chunk_samples != 2400 && chunk_samples != 3200)
+    return fail(TONE_E_INVALID, "chunk_samples must be 2400 (300 ms) or 3200 (400 ms), got " + std::to_string(chunk_samples));
+  s->geo = make_geom(chunk_samples);
+  return TONE_OK;
+}
+
+int tone_session_frames_per_chunk(const tone_session* s) { return s ? s->geo.T : 0; }
+
 int tone_session_set_graph(tone_session* s, int enable) {
   if (!s) return fail(TONE_E_INVALID, "null session");
   s->use_graph = enable != 0;
@@ -1026,11 +1041,11 @@ int tone_session_debug_read(tone_session* s, const char* buffer, void* host_dst,
   const std::string n(buffer);
   const float* p = nullptr;
   size_t cap = 0;
-  if (n == "feats") { p = s->feats; cap = MB * kMelT * kMels; }
-  else if (n == "x2") { p = static_cast<const float*>(s->x2); cap = MB * kSub2In * kSub1F * kSub1C; }
-  else if (n == "flat") { p = static_cast<const float*>(s->flat); cap = MB * kT * kSubOut; }
-  else if (n == "rA") { p = s->rA; cap = MB * kT * kD; }
-  else if (n == "rB") { p = s->rB; cap = MB * (kT / 2) * kD; }
+  if (n == "feats") { p = s->feats; cap = MB * kMelTMax * kMels; }
+  else if (n == "x2") { p = static_cast<const float*>(s->x2); cap = MB * kSub2InMax * kSub1F * kSub1C; }
+  else if (n == "flat") { p = static_cast<const float*>(s->flat); cap = MB * kTMax * kSubOut; }
+  else if (n == "rA") { p = s->rA; cap = MB * kTMax * kD; }
+  else if (n == "rB") { p = s->rB; cap = MB * kTrMax * kD; }
   else return fail(TONE_E_INVALID, "unknown debug buffer " + n);
   if ((size_t)bytes > cap * sizeof(float)) return fail(TONE_E_INVALID, "debug_read larger than the buffer");
   HIP_TRY(hipSetDevice(s->device));

@@ -33,7 +33,9 @@ class ToneSession:
     """One libtonehip session on one GPU: folded weights + activations resident in HBM."""
 
     def __init__(self, weights: dict, device: int = 0, precision: str = "fp32", max_batch: int = 256,
-                 graph: bool = False):
+                 graph: bool = False, chunk_samples: int = C.AUDIO_CHUNK_SAMPLES):
+        """``chunk_samples``: 2400 (300 ms, the reference's StreamingCTCModel) or 3200 (400 ms, the
+        Triton ensemble's chunk; 13 frames per step).  Same flat state in both."""
         torch = _torch()
         lib = _lib.load()
         if precision not in _lib.PRECISION:
@@ -53,6 +55,9 @@ class ToneSession:
             a = np.ascontiguousarray(arr, dtype=np.float32)
             _lib.check(lib.tone_session_set_weight(h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), a.size),
                        f"tone_session_set_weight({name})")
+        _lib.check(lib.tone_session_set_chunk(h, int(chunk_samples)), "tone_session_set_chunk")
+        self.chunk_samples = int(chunk_samples)
+        self.frames = int(lib.tone_session_frames_per_chunk(h))
         _lib.check(lib.tone_session_finalize(h), "tone_session_finalize")
         if graph:
             _lib.check(lib.tone_session_set_graph(h, 1), "tone_session_set_graph")
@@ -60,7 +65,7 @@ class ToneSession:
 
     # --- raw device-pointer step --------------------------------------------------------------
     def run(self, signal, state_in, logprobs, state_out, stream=None) -> None:
-        """signal int32 (B,2400[,1]), state_in/state_out fp16 (B, >=219729), logprobs fp32 (B,10,35);
+        """signal int32 (B, chunk[,1]), state_in/state_out fp16 (B, >=219729), logprobs fp32 (B, frames, 35);
         all contiguous torch tensors on this session's device."""
         torch = _torch()
         b = int(signal.shape[0])
@@ -72,6 +77,10 @@ class ToneSession:
             raise ValueError("state tensors must be row-contiguous with equal row strides")
         if not signal.is_contiguous() or not logprobs.is_contiguous():
             raise ValueError("signal and logprobs must be contiguous")
+        if signal.numel() != b * self.chunk_samples or logprobs.numel() < b * self.frames * C.VOCAB:
+            raise ValueError(f"signal must hold (B, {self.chunk_samples}) samples and logprobs (B, {self.frames}, 35)")
+        if not 0 < b <= self.max_batch:
+            raise ValueError(f"batch {b} outside 1..{self.max_batch}")
         st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
         _lib.check(self._lib.tone_session_run(self._h, signal.data_ptr(), state_in.data_ptr(), logprobs.data_ptr(),
                                               state_out.data_ptr(), b, state_in.stride(0), st),
@@ -103,9 +112,9 @@ class ToneSession:
             raise ValueError(f"batch {b} outside 1..{self.max_batch}")
         if tuple(slots.shape) != (b,) or not slots.is_contiguous():
             raise ValueError(f"slots must be a contiguous (B,) = ({b},) int32 tensor, got {tuple(slots.shape)}")
-        if signal.dim() < 2 or signal.shape[1] != C.AUDIO_CHUNK_SAMPLES or not signal.is_contiguous():
-            raise ValueError(f"signal must be a contiguous (B, {C.AUDIO_CHUNK_SAMPLES}) int32 tensor")
-        if not logprobs.is_contiguous() or logprobs.numel() < b * C.CHUNK_FRAMES * C.VOCAB:
+        if signal.dim() < 2 or signal.shape[1] != self.chunk_samples or not signal.is_contiguous():
+            raise ValueError(f"signal must be a contiguous (B, {self.chunk_samples}) int32 tensor")
+        if not logprobs.is_contiguous() or logprobs.numel() < b * self.frames * C.VOCAB:
             raise ValueError("logprobs must be contiguous with room for (B, 10, 35)")
         if slab_in.dim() != 2 or slab_out.shape != slab_in.shape or slab_in.stride(1) != 1 or slab_out.stride(1) != 1 \
                 or slab_in.stride(0) != slab_out.stride(0) or slab_in.stride(0) < C.STATE_SIZE \
@@ -139,9 +148,9 @@ class ToneSession:
         for r in (rows_in, rows_out):
             if tuple(r.shape) != (b,) or not r.is_contiguous():
                 raise ValueError(f"rows must be contiguous (B,) = ({b},) int32 tensors, got {tuple(r.shape)}")
-        if signal.dim() < 2 or signal.shape[1] != C.AUDIO_CHUNK_SAMPLES or not signal.is_contiguous():
-            raise ValueError(f"signal must be a contiguous (B, {C.AUDIO_CHUNK_SAMPLES}) int32 tensor")
-        if not logprobs.is_contiguous() or logprobs.numel() < b * C.CHUNK_FRAMES * C.VOCAB:
+        if signal.dim() < 2 or signal.shape[1] != self.chunk_samples or not signal.is_contiguous():
+            raise ValueError(f"signal must be a contiguous (B, {self.chunk_samples}) int32 tensor")
+        if not logprobs.is_contiguous() or logprobs.numel() < b * self.frames * C.VOCAB:
             raise ValueError("logprobs must be contiguous with room for (B, 10, 35)")
         if slab.dim() != 2 or slab.stride(1) != 1 or slab.stride(0) < C.STATE_SIZE or slab.shape[1] < C.STATE_SIZE:
             raise ValueError("slab must be (n_rows, >= 219729) fp16 with unit column stride")
@@ -165,8 +174,8 @@ class ToneSession:
         if frame_info is not None:
             if frame_info.dtype != torch.int32 or frame_info.device != self.dev or not frame_info.is_contiguous():
                 raise ValueError(f"frame_info must be a contiguous int32 tensor on {self.dev}")
-            if frame_info.numel() < self.max_batch * C.CHUNK_FRAMES:
-                raise ValueError(f"frame_info needs >= {self.max_batch * C.CHUNK_FRAMES} elements")
+            if frame_info.numel() < self.max_batch * self.frames:
+                raise ValueError(f"frame_info needs >= {self.max_batch * self.frames} elements")
             ptr = frame_info.data_ptr()
         self._frame_info = frame_info
         _lib.check(self._lib.tone_session_set_frame_info(self._h, ptr), "tone_session_set_frame_info")
@@ -178,7 +187,7 @@ class ToneSession:
         if state is None:
             state = torch.zeros((b, C.STATE_SIZE), dtype=torch.float16, device=self.dev)
         out_state = torch.empty_like(state)
-        logp = torch.empty((b, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=self.dev)
+        logp = torch.empty((b, self.frames, C.VOCAB), dtype=torch.float32, device=self.dev)
         self.run(signal.contiguous(), state, logp, out_state)
         return logp, out_state
 

@@ -177,3 +177,40 @@ def test_fp16_graph_delta_is_stated(oracle):
         worst = max(worst, float(np.abs(lp - ref).max()))
         np.testing.assert_array_equal(lp.argmax(-1), ref.argmax(-1))
     assert 1e-3 < worst < 2.5e-2, worst
+
+
+# ---- the 400 ms chunk variant, pinned to forward_for_export (tests/golden/make_golden_400ms.py) ----------
+def test_oracle_400ms_step_matches_forward_for_export():
+    """3200-sample chunk from a carried state: 40 mel frames, 13 frames, 6 in the reduced block, the
+    upsampling pad frame live; every stage within 2e-5, logprobs within 5e-5, next state within one
+    fp16 ulp (or 8e-6) with >= 99.5 % bit-identical (the bounds of the 300 ms pin above)."""
+    g = np.load(GOLDEN / "golden_400ms.npz")
+    orc = ToneOracle(synthetic_weights(0), round_feats=False)
+    trace = []
+    lp, st = orc.step(g["pcm"][:, 3].astype(np.int32), g["step_state_in"], trace=trace)
+    assert lp.shape == (4, 13, 35)
+    for i, t in enumerate(trace[1:]):
+        ref = g["step_stages"][:, i, : t.shape[1]]
+        assert t.shape[1] == (6 if 7 <= i <= 14 else 13), (i, t.shape)
+        assert np.abs(t - ref).max() < 2e-5, f"stage {i}: {np.abs(t - ref).max():.3g}"
+    assert np.abs(lp - g["step_logprobs"]).max() < 5e-5
+    ss = int(g["state_sample"])
+    got, ref = st[:, ::ss].astype(np.float32), g["step_state_out"].astype(np.float32)
+    d = np.abs(got - ref)
+    assert np.all(d <= np.maximum(np.abs(np.spacing(g["step_state_out"])).astype(np.float32), 8e-6))
+    assert np.mean(d == 0) >= 0.995
+
+
+def test_oracle_400ms_stream_matches_forward_for_export():
+    """4 streams x 5 chunks of 400 ms with staggered restarts (mhsa_len 0 / 13 / 26 / 30 in one batch)."""
+    g = np.load(GOLDEN / "golden_400ms.npz")
+    pcm = g["pcm"].astype(np.int32)
+    B, N = pcm.shape[:2]
+    orc = ToneOracle(synthetic_weights(0), round_feats=False)
+    st = np.zeros((B, C.STATE_SIZE), np.float16)
+    for c in range(N):
+        st[np.arange(B) > c] = 0
+        lp, st = orc.step(pcm[:, c], st)
+        ref = g["logprobs"][:, c]
+        assert np.abs(lp - ref).max() < 3e-4, (c, np.abs(lp - ref).max())
+        np.testing.assert_array_equal(lp.argmax(-1), ref.argmax(-1))
