@@ -39,9 +39,12 @@ GEMM_FAMILIES = ["gemm_ffn_up", "gemm_ffn_down", "gemm_qkv", "gemm_attn_out", "g
                  "gemm_sub_out", "gemm_reduce"]
 
 
-def family_flops_per_stream() -> dict:
+def family_flops_per_stream(T: int = C.CHUNK_FRAMES) -> dict:
+    """Algorithmic FLOP per stream-chunk of each GEMM family; T = 10 (300 ms) or 13 (400 ms) frames,
+    Tr = (T + 1 - 3) // 2 + 1 inside the reduced block (layers 7..14)."""
     d, ff = C.D_MODEL, C.D_FF
-    frames = [C.layer_frames(l) for l in range(C.N_LAYERS)]
+    tr = (T + 1 - 3) // 2 + 1
+    frames = [tr if C.REDUCTION_POS < l <= C.UPSAMPLE_POS else T for l in range(C.N_LAYERS)]
     f = {k: 0 for k in GEMM_FAMILIES}
     for l, t in enumerate(frames):
         f["gemm_ffn_up"] += 2 * (2 * t * d * 2 * ff)
@@ -54,8 +57,8 @@ def family_flops_per_stream() -> dict:
         f["gemm_attn_out"] += 2 * t * d * d
         f["gemm_pw1"] += 2 * t * d * 2 * d
         f["gemm_pw2"] += 2 * t * d * d
-    f["gemm_sub_out"] = 2 * 10 * C.SUB_OUT_IN * d
-    f["gemm_reduce"] = 2 * 5 * 4 * d * d
+    f["gemm_sub_out"] = 2 * T * C.SUB_OUT_IN * d
+    f["gemm_reduce"] = 2 * tr * 4 * d * d
     return f
 
 
@@ -86,9 +89,9 @@ def algo_bytes(family: str, precision: str, batch: int) -> float:
     return sum(per) / len(per)
 
 
-def synthetic_pcm(rng, b, n_chunks, silence=0.2):
+def synthetic_pcm(rng, b, n_chunks, silence=0.2, chunk=C.AUDIO_CHUNK_SAMPLES):
     """Gaussian sigma=3000 clipped to int16, 20 % silent chunks."""
-    x = np.clip(np.round(rng.normal(0.0, 3000.0, size=(n_chunks, b, C.AUDIO_CHUNK_SAMPLES))), -32768, 32767)
+    x = np.clip(np.round(rng.normal(0.0, 3000.0, size=(n_chunks, b, chunk))), -32768, 32767)
     x[rng.random((n_chunks, b)) < silence] = 0
     return x.astype(np.int32)
 
@@ -138,7 +141,7 @@ def replica_weights(pg, dev):
     return _WEIGHTS
 
 
-def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True, cap=None):
+def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True, cap=None, chunk=C.AUDIO_CHUNK_SAMPLES):
     """Time args.steps streaming steps of B streams on this GPU; returns a dict with the max-over-ranks
     elapsed time, per-step percentiles (HIP events on the launch stream) and the roofline (rank 0).
 
@@ -148,13 +151,14 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
     shards so the collective has equal parts."""
     cap = cap or B
     sess = ToneSession(replica_weights(pg, dev), device=local, precision=precision, max_batch=B,
-                       graph=not args.no_graph)
+                       graph=not args.no_graph, chunk_samples=chunk)
+    fr = sess.frames
     rng = np.random.default_rng(1000 + rank)
-    pcm = torch.from_numpy(synthetic_pcm(rng, B, args.chunks)).to(dev)             # (chunks, B, 2400)
+    pcm = torch.from_numpy(synthetic_pcm(rng, B, args.chunks, chunk=chunk)).to(dev)   # (chunks, B, chunk)
     slabs = [torch.zeros((B, C.STATE_SIZE), dtype=torch.float16, device=dev) for _ in range(2)]
-    signal = torch.empty((B, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32, device=dev)   # audio lands here
-    logp = [torch.zeros((cap, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev) for _ in range(2)]
-    gathered = [torch.empty((world * cap, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev)
+    signal = torch.empty((B, chunk), dtype=torch.int32, device=dev)   # audio lands here
+    logp = [torch.zeros((cap, fr, C.VOCAB), dtype=torch.float32, device=dev) for _ in range(2)]
+    gathered = [torch.empty((world * cap, fr, C.VOCAB), dtype=torch.float32, device=dev)
                 for _ in range(2)] if pg is not None else None
     stream = torch.cuda.Stream(dev)
     comm = torch.cuda.Stream(dev) if pg is not None else None
@@ -172,7 +176,7 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
                 comm.wait_event(ready)
                 if args.dist_backend == "gloo":      # one-GPU rehearsal: gloo gathers host tensors
                     comm.synchronize()
-                    host = torch.empty((world * cap, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32)
+                    host = torch.empty((world * cap, fr, C.VOCAB), dtype=torch.float32)
                     pg.all_gather_into_tensor(host, logp[k].cpu())
                     gathered[k].copy_(host)
                 else:
@@ -217,7 +221,7 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
                 signal.copy_(pcm[i % args.chunks], non_blocking=True)
                 sess.run(signal, slabs[i % 2], logp[0][:B], slabs[(i + 1) % 2], stream=stream)
         torch.cuda.synchronize()
-        per_stream = family_flops_per_stream()
+        per_stream = family_flops_per_stream(fr)
         fams = {}
         for fam in GEMM_FAMILIES:
             us, n = sess.kernel_us(fam)
@@ -229,17 +233,18 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
         f = fams[dom]
         achieved = f["flop_per_launch"] / (f["avg_us"] * 1e-6) / 1e12
         peak = PEAK_TFLOPS[precision]
-        traffic, tsrc = measured_traffic(dom, precision, B)
+        traffic, tsrc = measured_traffic(dom, precision, B) if chunk == 2400 else (None, None)
         gemm_us = sum(v["avg_us"] * v["launches_per_step"] for v in fams.values())
         gemm_flop = sum(per_stream.values()) * B
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": tsrc, "algo_bytes": int(algo_bytes(dom, precision, B)),
+                "traffic_source": tsrc, "algo_bytes": int(algo_bytes(dom, precision, B)) if chunk == 2400 else None,
                 "avg_us": round(f["avg_us"], 2), "flop_per_launch": int(f["flop_per_launch"]),
-                "step_tflops": round(C.FLOP_PER_CHUNK * B / (elapsed / args.steps) / 1e12, 2),
+                "step_tflops": round(C.FLOP_PER_CHUNK * B / (elapsed / args.steps) / 1e12, 2) if chunk == 2400 else None,
                 "encoder_gemm_tflops": round(gemm_flop / (gemm_us * 1e-6) / 1e12, 2),
                 "encoder_gemm_frac": round(gemm_flop / (gemm_us * 1e-6) / 1e12 / peak, 4),
-                "step_io_gbs": round(B * C.IO_BYTES_PER_CHUNK / (elapsed / args.steps) / 1e9, 1),
+                "step_io_gbs": round(B * (C.IO_BYTES_PER_CHUNK + 4 * (chunk - 2400) + 4 * (fr - 10) * 35)
+                                     / (elapsed / args.steps) / 1e9, 1),
                 "families_us_per_step": {k: round(v["avg_us"] * v["launches_per_step"], 1) for k, v in fams.items()}}
         if precision == "fp32":
             roof["gemm_arith"] = ("fp32 as exact 3-way bf16 splits, 6 products per multiply-add on "
@@ -253,11 +258,12 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
     return res
 
 
-def workload_line(name, res, n_streams, steps, dtype, **extra):
+def workload_line(name, res, n_streams, steps, dtype, chunk=C.AUDIO_CHUNK_SAMPLES, **extra):
     dt = res["elapsed"] / steps
-    return {"workload": name, "value": round(n_streams / dt * C.AUDIO_CHUNK_SAMPLES / C.SAMPLE_RATE, 1),
+    chunk_ms = chunk * 1000.0 / C.SAMPLE_RATE
+    return {"workload": name, "value": round(n_streams / dt * chunk / C.SAMPLE_RATE, 1),
             "unit": "real-time streams", "ms_per_step": round(dt * 1e3, 4), "median_ms": res["median_ms"],
-            "p99_ms": res["p99_ms"], "chunks_per_s": round(n_streams / dt, 1), "rtf": round(dt * 1e3 / 300.0, 5),
+            "p99_ms": res["p99_ms"], "chunks_per_s": round(n_streams / dt, 1), "rtf": round(dt * 1e3 / chunk_ms, 5),
             "dtype": dtype, **extra, "roofline": res["roofline"]}
 
 
@@ -276,7 +282,8 @@ def main() -> None:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse N > 1 on one GPU (ranks share the card, collectives staged through host)")
-    ap.add_argument("--alt", type=int, default=1, help="also measure BASELINE config 3 (bf16, B=2048) at N=1")
+    ap.add_argument("--alt", type=int, default=1, help="also measure BASELINE config 3 (bf16, B=2048) and the 400 ms "
+                                                       "variant (fp32, B=256) at N=1")
     ap.add_argument("--config4", type=int, default=4096,
                     help="also measure BASELINE config 4: this many streams in total, sharded over the N GPUs, "
                          "bf16, logprobs all-gathered (0 = skip)")
@@ -320,6 +327,11 @@ def main() -> None:
         r2 = measure(args, 2048, "bf16", dev, local, world, rank, pg)
         alts.append(workload_line("BASELINE config 3: streaming step, batch 2048, bf16 MFMA GEMMs, stateful 300 ms "
                                   "chunks", r2, 2048, args.steps, "bf16", n_gpus=1, scaling="n/a"))
+        # the 400 ms chunk variant (3200 samples -> 13 frames), config 2's batch and dtype
+        r400 = measure(args, 256, "fp32", dev, local, world, rank, pg, chunk=3200)
+        alts.append(workload_line("400 ms chunk variant: streaming step, batch 256, fp32, stateful 3200-sample chunks "
+                                  "(13 frames per step)", r400, 256, args.steps, "fp32", chunk=3200, n_gpus=1,
+                                  scaling="n/a"))
     # BASELINE config 4 (4096 streams over the node's GPUs, strong scaling, RCCL all-gather of logprobs)
     if args.config4 and not (args.global_batch == args.config4 and args.precision == "bf16"):
         sizes = shard_sizes(args.config4, world)

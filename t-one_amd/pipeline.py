@@ -142,7 +142,7 @@ class StreamingGreedyPipeline:
     greedy tokens (10 ids + 10 bits per stream-chunk cross PCIe).
     """
 
-    CHUNK_SIZE = C.AUDIO_CHUNK_SAMPLES
+    CHUNK_SIZE = C.AUDIO_CHUNK_SAMPLES   # 300 ms; a session built with chunk_samples=3200 serves 400 ms chunks
 
     def __init__(self, session, n_slots: int, decoder=None):
         import torch
@@ -150,6 +150,8 @@ class StreamingGreedyPipeline:
             raise ValueError("n_slots must be positive")
         self.session = session
         self.n_slots = int(n_slots)
+        self.CHUNK_SIZE = int(getattr(session, "chunk_samples", C.AUDIO_CHUNK_SAMPLES))
+        self.frames = fr = int(getattr(session, "frames", C.CHUNK_FRAMES))
         dev = session.dev
         self._slab = torch.zeros((2 * self.n_slots, STATE_STRIDE), dtype=torch.float16, device=dev)
         self._parity = np.zeros(self.n_slots, np.int32)
@@ -157,15 +159,15 @@ class StreamingGreedyPipeline:
         self._free = list(range(self.n_slots - 1, -1, -1))
         mb = session.max_batch
         # fixed staging buffers: the device pointers stay the same across steps (hipGraph friendly)
-        self._info = torch.zeros((mb, C.CHUNK_FRAMES), dtype=torch.int32, device=dev)
-        self._logp = torch.empty((mb, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32, device=dev)
-        self._sig = torch.zeros((mb, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32, device=dev)
+        self._info = torch.zeros((mb, fr), dtype=torch.int32, device=dev)
+        self._logp = torch.empty((mb, fr, C.VOCAB), dtype=torch.float32, device=dev)
+        self._sig = torch.zeros((mb, self.CHUNK_SIZE), dtype=torch.int32, device=dev)
         self._rows = torch.zeros((2, mb), dtype=torch.int32, device=dev)
-        self._sig_h = torch.zeros((mb, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32).pin_memory()
+        self._sig_h = torch.zeros((mb, self.CHUNK_SIZE), dtype=torch.int32).pin_memory()
         self._rows_h = torch.zeros((2, mb), dtype=torch.int32).pin_memory()
-        self._info_h = torch.zeros((mb, C.CHUNK_FRAMES), dtype=torch.int32).pin_memory()
+        self._info_h = torch.zeros((mb, fr), dtype=torch.int32).pin_memory()
         self.decoder = decoder
-        self._logp_h = torch.zeros((mb, C.CHUNK_FRAMES, C.VOCAB), dtype=torch.float32).pin_memory() \
+        self._logp_h = torch.zeros((mb, fr, C.VOCAB), dtype=torch.float32).pin_memory() \
             if decoder is not None else None
         self._last_logp: Optional[np.ndarray] = None
 
@@ -206,8 +208,8 @@ class StreamingGreedyPipeline:
         import torch
         n = len(slots)
         mb = self.session.max_batch
-        info = np.empty((n, C.CHUNK_FRAMES), np.int32)
-        logp = np.empty((n, C.CHUNK_FRAMES, C.VOCAB), np.float32) if self.decoder is not None else None
+        info = np.empty((n, self.frames), np.int32)
+        logp = np.empty((n, self.frames, C.VOCAB), np.float32) if self.decoder is not None else None
         self.session.set_frame_info(self._info)    # frame_info is session state: claim it every step
         for b0 in range(0, n, mb):
             b1 = min(n, b0 + mb)
@@ -247,7 +249,7 @@ class StreamingGreedyPipeline:
         if len(set(slots)) != n or any(s not in self._open for s in slots):
             raise ValueError("slots must be distinct open stream slots")
         is_last = [False] * n if is_last is None else list(is_last)
-        info = self.step_frames(chunks, slots) if n else np.zeros((0, C.CHUNK_FRAMES), np.int32)
+        info = self.step_frames(chunks, slots) if n else np.zeros((0, self.frames), np.int32)
         out: list[list[TextPhrase]] = []
         for i, slot in enumerate(slots):
             toks, speech = decode_frame_info(info[i])
@@ -317,8 +319,9 @@ class StreamScheduler:
 
     def submit(self, stream_id, chunk: np.ndarray, is_last: bool = False) -> None:
         chunk = np.asarray(chunk)
-        if chunk.shape != (C.AUDIO_CHUNK_SAMPLES,) or chunk.dtype != np.int32:
-            raise ValueError(f"chunk must be int32 ({C.AUDIO_CHUNK_SAMPLES},), got {chunk.dtype} {chunk.shape}")
+        size = getattr(self.pipe, "CHUNK_SIZE", C.AUDIO_CHUNK_SAMPLES)
+        if chunk.shape != (size,) or chunk.dtype != np.int32:
+            raise ValueError(f"chunk must be int32 ({size},), got {chunk.dtype} {chunk.shape}")
         if stream_id not in self._slot:
             self._slot[stream_id] = self.pipe.open_stream()
             self._queues[stream_id] = self._deque()
