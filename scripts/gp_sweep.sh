@@ -3,7 +3,7 @@ set -u
 mkdir -p gpurun_out
 out=gpurun_out/gp_sweep.log
 : > $out
-V=${V:-20,90,92,93}
+V=${V:-20,24,90,92,94,95}
 run() { timeout -k 10 120 ./t-one_amd/gemm_bench "$@" >> $out 2>&1 || { echo "rc=$? on $*"; cat $out; exit 1; }; }
 export ROWSCALE=1
 for r in 1 2; do

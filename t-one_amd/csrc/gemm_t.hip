@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_t_kernel(GemmArgs p
 //   * the folded-RMSNorm row scale is computed by every wave from its own X fragments (no LDS).
 // Phases of one K-tile (each 16 MFMAs): (n 0-63, m 0-31), (n 0-63, m 32-63), (n 64-127, m 32-63),
 // (n 64-127, m 0-31) of the wave tile.  LDS: 2 x 64 KiB stages + the bias vector.
-template <int EPI, bool RS, bool PRIO, int DBG = 0, int STK = 0>
+template <int EPI, bool RS, bool PRIO, int DBG = 0, int STK = 0, int ROT = 0>
 __global__ void __launch_bounds__(512) gemm_p_kernel(GemmArgs p) {
   constexpr int BK = 64, QB = 128 * BK, STG = 4 * QB;
   constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
@@ -367,7 +367,10 @@ __global__ void __launch_bounds__(512) gemm_p_kernel(GemmArgs p) {
     if constexpr ((DBG & 4) != 0) return;                       // microbenchmark: no staging
     int m0, n0;
     tile_of(u, m0, n0);
-    const int k0 = (u % nk) * BK;
+    // ROT: each tile walks its K-tiles from a different start (the tile index mod nk), so the CUs that
+    // stream the same X rows / W rows at the same time ask for different 128-byte lines
+    const int rot = ROT ? (tbeg + jb + (u / nk) * nxb) % nk : 0;
+    const int k0 = ((u % nk + rot) % nk) * BK;
     uint16_t* dst = lds + (u & 1) * STG + j * QB;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1283,16 +1286,16 @@ hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st) {
 }
 
 // Tile variants: 0 = 256x256 (waves 2x4), 1 = 128x256 (2x4), 2 = 256x128 (2x4), 3 = 128x128 (2x4)
-template <int EPI, bool PRIO, int STK = 0>
+template <int EPI, bool PRIO, int STK = 0, int ROT = 0>
 hipError_t launch_p(const GemmArgs& a, hipStream_t st) {
   const int ntiles = (a.N / 256) * ((a.M + 255) / 256);
   int grid = num_cus_t();
   const int need = ((ntiles + 7) / 8) * 8;
   if (grid > need) grid = need;
   grid = (grid + 7) / 8 * 8;
-  if constexpr (STK != 0) {
-    if (a.rowscale) hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 0, STK>), dim3(grid), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((gemm_p_kernel<EPI, false, PRIO, 0, STK>), dim3(grid), dim3(512), 0, st, a);
+  if constexpr (STK != 0 || ROT != 0) {
+    if (a.rowscale) hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 0, STK, ROT>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((gemm_p_kernel<EPI, false, PRIO, 0, STK, ROT>), dim3(grid), dim3(512), 0, st, a);
     return hipGetLastError();
   }
   if constexpr (EPI == EPI_SWIGLU && !PRIO) {   // microbenchmark ablations (tools/gemm_bench, dbg bits)
@@ -1312,7 +1315,7 @@ hipError_t launch_p(const GemmArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <bool PRIO, int STK = 0>
+template <bool PRIO, int STK = 0, int ROT = 0>
 hipError_t launch_p_epi(const GemmArgs& a, int epi, hipStream_t st) {
   if (!a.a_bf16 || a.N % 256 || a.K % 64 || a.N > kBiasMax || a.rpg || a.M <= 0 || a.c_plane || a.c2_plane ||
       (a.ldc % 4) || (a.lda % 8))
@@ -1320,8 +1323,8 @@ hipError_t launch_p_epi(const GemmArgs& a, int epi, hipStream_t st) {
   switch (epi) {
     case EPI_STORE: return launch_p<EPI_STORE, PRIO>(a, st);
     case EPI_RESID: return a.c_bf16 ? hipErrorInvalidValue : launch_p<EPI_RESID, PRIO>(a, st);
-    case EPI_SWIGLU: return launch_p<EPI_SWIGLU, PRIO, STK>(a, st);
-    case EPI_GLU: return launch_p<EPI_GLU, PRIO, STK>(a, st);
+    case EPI_SWIGLU: return launch_p<EPI_SWIGLU, PRIO, STK, ROT>(a, st);
+    case EPI_GLU: return launch_p<EPI_GLU, PRIO, STK, ROT>(a, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1334,6 +1337,8 @@ hipError_t gemm_p(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     case 1: return launch_p_epi<true>(a, epi, st);
     case 2: return launch_p_epi<false, 1>(a, epi, st);
     case 3: return launch_p_epi<false, 2>(a, epi, st);
+    case 4: return launch_p_epi<false, 0, 1>(a, epi, st);   // K-tile rotation per tile
+    case 5: return launch_p_epi<false, 1, 1>(a, epi, st);
     default: return hipErrorInvalidValue;
   }
 }
