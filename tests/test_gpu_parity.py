@@ -437,3 +437,29 @@ def test_fp32_pre_encode_split_vs_mfma(weights, oracle):
     print("pre-encode relative L2 error:", rel)
     assert rel["fp32"] < 1e-4, rel
     assert rel["fp32"] <= 2 * rel["fp32-mfma"] + 1e-6, rel
+
+
+def test_hip_vs_forward_for_export(sess):
+    """The HIP fp32 path on the golden streams (4 x 6 chunks, staggered restarts) against the reference's
+    own Tone.forward_for_export (tests/golden/golden_fx.npz), argmax identical to both of its modes.
+    * fp32 mode of the golden (fp16 states, features NOT rounded to fp16): the HIP path rounds the
+      features to fp16 at the ONNX boundary (the export's fp16 `signal` path), and that rounding point alone
+      moves the logprobs by 1.85e-3 -- the oracle with the same rounding differs from this golden by
+      1.854e-3, the HIP path by 1.868e-3 (measured on the MI355X).  Bound 2.5e-3; the 1e-3 arithmetic bar
+      is held against the oracle with identical rounding points (test_golden_stream, <= 1e-3).
+    * fp16-autocast graph (the ONNX export's semantics, tone/scripts/export.py:411): the stated 2.5e-2
+      fp16-graph delta (tests/test_oracle.py; measured 1.58e-2)."""
+    g, gs = np.load(GOLDEN / "golden_fx.npz"), np.load(GOLDEN / "golden_stream.npz")
+    pcm = gs["pcm"].astype(np.int32)
+    B, N = pcm.shape[:2]
+    st = np.zeros((B, C.STATE_SIZE), np.float16)
+    d32 = d16 = 0.0
+    for c in range(N):
+        st[np.arange(B) > c] = 0
+        lp, st = gpu_step(sess, pcm[:, c], st)
+        r32, r16 = g["stream_fp32_logprobs"][:, c], g["stream_fp16_logprobs"][:, c]
+        d32, d16 = max(d32, float(np.abs(lp - r32).max())), max(d16, float(np.abs(lp - r16).max()))
+        np.testing.assert_array_equal(lp.argmax(-1), r32.argmax(-1))
+        np.testing.assert_array_equal(lp.argmax(-1), r16.argmax(-1))
+    print(f"HIP fp32 vs forward_for_export: fp32 {d32:.3g}, fp16-autocast {d16:.3g}")
+    assert d32 < 2.5e-3 and d16 < 2.5e-2, (d32, d16)
