@@ -1060,6 +1060,11 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     // fp32 by exact bf16 splitting (gemm_t.hip gemm_x3); tile per shape from tools/gemm_bench
     // (scripts/x3_sweep.sh, profiles/r01_x3_sweep_b256.jsonl)
     // (scripts/x3_sweep.sh, scripts/x3w_sweep.sh; profiles/r01_x3_*.jsonl)
+    // k|v of layers 14 / 15 (M = B (S + T) >= 5120 at B = 256, N = 768): fp32 W and X through the K-tile
+    // ring (gemm_r3) -- 48.8 vs 77.5 us at M = 10240, 33.5 vs 39.8 at 5120; on every other shape of the
+    // step the ring kernel is slower (profiles/r02_r3_sweep.jsonl)
+    if (epi == EPI_STORE && a.N == 768 && a.M >= 4096 && a.W && !a.rowscale)
+      return gemm_r3(a, epi, a.M >= 8192 ? 0 : 1, st);
     if (epi == EPI_SWIGLU && a.N % 256 == 0)
       return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200 ? 7 : 6, st);
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);

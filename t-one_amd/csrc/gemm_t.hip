@@ -1182,6 +1182,297 @@ hipError_t launch_x3_epi(const GemmArgs& a, int epi, hipStream_t st) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 projections by exact splitting, both operands streamed as fp32 ("r3": K-tile ring).
+//
+// gemm_x3 stages W as its three bf16 planes (6 bytes per element) and X as fp32.  Here W is staged as
+// fp32 too (4 bytes, split in registers like X): 4 (BN + BM) bytes per k instead of (6 BN + 4 BM), and
+// the stages form a ring of R K-tiles (32 k = one 128-byte line per row) with up to R - 1 in flight.
+//   * persistent over tiles, the ring runs across tile boundaries; tiles dealt XCD-contiguously;
+//   * per wave and 16-deep half: the raw fp32 fragments of W and X are read (two ds_read_b128 per
+//     row and lane, slot ^= (row >> 1) & 7 applied on the DMA source), split in registers into
+//     their three bf16 terms, and the six products with i + j <= 2 go to v_mfma_f32_32x32x16_bf16
+//     (the arithmetic of gemm_x3: fp32-accurate, see there);
+//   * folded RMSNorm (RS): the row sum of squares from the raw X fragments, as in gemm_x3.
+// Measured (tools/gemm_bench, scripts/r3_sweep.sh / r3_ablate.sh, profiles/r02_r3_*.jsonl): the ring's
+// DMA alone (no reads, split or MFMA) fills at 38-48 GB/s per CU, and the extra split VALU costs more
+// than the saved bytes on every B = 256 shape except the large-M k|v projections of layers 14 / 15,
+// which is where gemm() routes it.
+template <int BN_, int BM_, int WN_, int WM_, int R_, int NB_>
+struct RT {
+  static constexpr int BN = BN_, BM = BM_, WN = WN_, WM = WM_, R = R_, NB = NB_;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(k * IPW) for a wave-uniform k in [0, KMAX]
+template <int IPW, int KMAX>
+__device__ __forceinline__ void wait_vm_tiles(int k) {
+  if constexpr (KMAX >= 4) if (k >= 4) { wait_vm_n<4 * IPW>(); return; }
+  if constexpr (KMAX >= 3) if (k == 3) { wait_vm_n<3 * IPW>(); return; }
+  if constexpr (KMAX >= 2) if (k == 2) { wait_vm_n<2 * IPW>(); return; }
+  if constexpr (KMAX >= 1) if (k == 1) { wait_vm_n<IPW>(); return; }
+  wait_vm_n<0>();
+}
+
+// Software pipeline (one wave's instruction stream): the MFMAs of one 16-deep half run on operands
+// split in the previous phase while the LDS reads and the split of the next half are issued between
+// them, so the VALU and the LDS-DMA issue fill the MFMA shadow instead of following it:
+//   phase A of K-tile t:  MFMA(t, h0)  ||  read + split (t, h1)
+//   wait K-tile t + 1, barrier (every wave is past its reads of K-tile t), DMA K-tile t + R into t's slot
+//   phase B of K-tile t:  MFMA(t, h1)  ||  read + split (t + 1, h0)
+// The issue and read indices are clamped to the last K-tile, so every phase is branch-free and the
+// barrier waits on a fixed vmcnt; the ring slots those clamped DMAs land in are never read again.
+// DBG (microbenchmark ablations only): bit 0 no MFMA, bit 1 no split (fragments reinterpreted), bit 2 no
+// LDS-DMA, bit 3 no epilogue; every accumulator stays live
+template <class TL, int EPI, bool RS, int DBG = 0>
+__global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_r3_kernel(GemmArgs p) {
+  constexpr int BN = TL::BN, BM = TL::BM, WN = TL::WN, WM = TL::WM, R = TL::R, NB = TL::NB;
+  constexpr int NW = WN * WM, NT = NW * 64;
+  constexpr int WTN = BN / WN, WTM = BM / WM, TI = WTN / 32, TJ = WTM / 32;
+  constexpr int STAGE = (BN + BM) * 32;                          // floats of one K-tile
+  constexpr int P = (BN + BM) / 8, IPW = P / NW;                 // 1 KiB pieces (8 rows x 128 B)
+  static_assert(P % NW == 0 && TI >= 1 && TJ >= 1 && WN >= TJ, "pieces per wave / tile ownership");
+  static_assert(R >= 3 && R <= 6 && (R - 2) * IPW <= 63, "ring depth / vmcnt range");
+  __shared__ __attribute__((aligned(16))) float lds[R * STAGE + NB + BM];
+  float* sbias = lds + R * STAGE;
+  float* rden = sbias + NB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid / WM, wm = wid % WM, lr = lane & 31, lh = lane >> 5;
+  const int ntn = p.N / BN, ntm = (p.M + BM - 1) / BM, ntiles = ntn * ntm;
+  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int q = (ntiles + 7) >> 3, tbeg = xcd * q, tend = min(ntiles, tbeg + q);
+  const int nmine = (tbeg + jb < tend) ? (tend - tbeg - jb + nxb - 1) / nxb : 0;
+  for (int i = tid; i < p.N; i += NT) sbias[i] = p.bias ? p.bias[i] : 0.f;
+  __syncthreads();
+  if (nmine <= 0) return;                                        // workgroup-uniform
+  const int nk = p.K / 32, G = nmine * nk;
+  const float* __restrict__ W = static_cast<const float*>(p.W);
+  const float* __restrict__ X = static_cast<const float*>(p.A);
+
+  auto tile_of = [&](int u, int& m0, int& n0) {
+    const int t = tbeg + jb + (u / nk) * nxb;
+    m0 = (t / ntn) * BM;
+    n0 = (t % ntn) * BN;
+  };
+  // per-lane source rows of this wave's pieces: W rows for pieces < BN / 8, X rows after
+  auto issue = [&](int u) {
+    if constexpr (DBG & 4) return;
+    int m0, n0;
+    tile_of(u, m0, n0);
+    const int k0 = (u % nk) * 32;
+    float* base = lds + (u % R) * STAGE;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int pc = wid + i * NW;                               // wave-uniform
+      const int r = pc * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const bool isw = pc < BN / 8;
+      const float* src = isw ? W + (int64_t)(n0 + r) * p.K : X + (int64_t)min(m0 + r - BN, p.M - 1) * p.lda;
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src + k0 + 4 * c, base + pc * 256, 16, 0, 0);
+#else
+      (void)src;
+      (void)base;
+#endif
+    }
+  };
+
+  struct Ops {
+    bf16x8 w0[TI], w1[TI], w2[TI], x0[TJ], x1[TJ], x2[TJ];
+  };
+  // raw fp32 fragments of half h of the K-tile in `slot` -> their bf16 terms; returns the lane's
+  // partial sum of squares of its X row (RS)
+  auto read_split = [&](int slot, int h, Ops& o) -> float {
+    if constexpr ((DBG & 16) != 0) return 0.f;                  // ablation: no LDS reads at all
+    const float* base = lds + slot * STAGE;
+    const int c0 = 4 * h + 2 * lh;                               // first 16-byte chunk of this lane's 8 k
+    f32x4 wv[TI][2], xv[TJ][2];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int row = wn * WTN + 32 * i + lr, s = (row >> 1) & 7;
+      wv[i][0] = *reinterpret_cast<const f32x4*>(base + row * 32 + ((c0 ^ s) << 2));
+      wv[i][1] = *reinterpret_cast<const f32x4*>(base + row * 32 + (((c0 + 1) ^ s) << 2));
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int row = BN + wm * WTM + 32 * j + lr, s = (row >> 1) & 7;
+      xv[j][0] = *reinterpret_cast<const f32x4*>(base + row * 32 + ((c0 ^ s) << 2));
+      xv[j][1] = *reinterpret_cast<const f32x4*>(base + row * 32 + (((c0 + 1) ^ s) << 2));
+    }
+    if constexpr (DBG & 2) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        o.w0[i] = __builtin_bit_cast(bf16x8, wv[i][0]); o.w1[i] = __builtin_bit_cast(bf16x8, wv[i][1]); o.w2[i] = o.w0[i];
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        o.x0[j] = __builtin_bit_cast(bf16x8, xv[j][0]); o.x1[j] = __builtin_bit_cast(bf16x8, xv[j][1]); o.x2[j] = o.x1[j];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) split3(wv[i][0], wv[i][1], o.w0[i], o.w1[i], o.w2[i]);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) split3(xv[j][0], xv[j][1], o.x0[j], o.x1[j], o.x2[j]);
+    }
+    float c = 0.f;
+    if constexpr (RS) {
+      const int jss = wn % TJ;                                   // m-tile whose sum of squares this wave keeps
+      f32x4 a = xv[0][0], b = xv[0][1];
+#pragma unroll
+      for (int j = 1; j < TJ; ++j) {
+        a = (jss == j) ? xv[j][0] : a;
+        b = (jss == j) ? xv[j][1] : b;
+      }
+      c = a.x * a.x; c = fmaf(a.y, a.y, c); c = fmaf(a.z, a.z, c); c = fmaf(a.w, a.w, c);
+      c = fmaf(b.x, b.x, c); c = fmaf(b.y, b.y, c); c = fmaf(b.z, b.z, c); c = fmaf(b.w, b.w, c);
+    }
+    return c;
+  };
+
+  f32x16 acc[TI][TJ];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  };
+  auto mfma = [&](const Ops& o) {
+    if constexpr (DBG & 1) {   // no MFMA: fold the operands into the accumulators (keeps them live)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j][0] += __builtin_bit_cast(f32x4, o.w2[i]).x + __builtin_bit_cast(f32x4, o.x2[j]).x +
+                          __builtin_bit_cast(f32x4, o.w1[i]).y + __builtin_bit_cast(f32x4, o.x1[j]).y +
+                          __builtin_bit_cast(f32x4, o.w0[i]).z + __builtin_bit_cast(f32x4, o.x0[j]).z;
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {   // small terms first
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.w2[i], o.x0[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.w1[i], o.x1[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.w0[i], o.x2[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.w1[i], o.x0[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.w0[i], o.x1[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.w0[i], o.x0[j], acc[i][j], 0, 0, 0);
+      }
+  };
+  // interleave hint for one phase: the LDS reads first, then MFMAs with the split VALU between them
+  auto interleave = [&]() {
+    constexpr int NM = (DBG & 1) ? 0 : 6 * TI * TJ;
+    if constexpr (NM > 0) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 * (TI + TJ), 0);   // ds_read_b128
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                // MFMA (reads in flight)
+#pragma unroll
+      for (int k = 2; k < NM; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x002, (TI + TJ) * 22 / (NM - 2) + 1, 0);   // VALU
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
+      }
+    }
+  };
+
+  zero();
+  float ss = 0.f, ss_next = 0.f;
+  for (int u = 0; u < R; ++u) issue(min(u, G - 1));             // the ring starts full
+  wait_vm_n<(R - 1) * IPW>();                                    // K-tile 0 landed (this wave's pieces)
+  barrier_lds();
+  Ops cur, nxt;
+  ss += read_split(0, 0, cur);
+  for (int t = 0; t < G; ++t) {
+    const int slot = t % R;
+    // phase A: MFMA (t, h0) || read + split (t, h1)
+    ss += read_split(slot, 1, nxt);
+    mfma(cur);
+    interleave();
+    cur = nxt;
+    // K-tile t + 1 landed: R - 2 later K-tiles stay in flight (clamped DMAs included)
+    wait_vm_n<(R - 2) * IPW>();
+    barrier_lds();                                               // every wave past its reads of K-tile t
+    issue(min(t + R, G - 1));                                    // into slot t % R
+    // phase B: MFMA (t, h1) || read + split (t + 1, h0)
+    const int tn = min(t + 1, G - 1);
+    const bool last = (t % nk == nk - 1);                        // K-tile t ends a tile: t + 1 starts the next
+    const float cn = read_split(tn % R, 0, nxt);
+    if (last) ss_next = cn; else ss += cn;
+    mfma(cur);
+    interleave();
+    cur = nxt;
+    if (last) {
+      int m0, n0;
+      tile_of(t, m0, n0);
+      if constexpr (RS) {
+        const float s2 = ss + __shfl_xor(ss, 32, 64);
+        if (wn < TJ && lh == 0) rden[wm * WTM + 32 * wn + lr] = sqrtf(s2) * p.inv_sqrt_k + kRmsEps;
+        barrier_lds();
+        ss = ss_next;
+      }
+      if constexpr (DBG & 8) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)   // never true (alpha is finite): keeps every accumulator live
+            if (p.alpha == -1.2345e30f) *reinterpret_cast<f32x16*>(static_cast<float*>(p.C) + 16 * (64 * (i * TJ + j) + lane)) = acc[i][j];
+      } else {
+        tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias + n0, m0, n0, wn, wm, lr, lh);
+      }
+      zero();
+    }
+  }
+  wait_vm_n<0>();                                                // no LDS-DMA outlives the workgroup
+}
+
+template <class TL, int EPI>
+hipError_t launch_r3(const GemmArgs& a, hipStream_t st) {
+  const int ntiles = (a.N / TL::BN) * ((a.M + TL::BM - 1) / TL::BM);
+  int grid = 256;                                                // one workgroup per CU (LDS)
+  const int need = ((ntiles + 7) / 8) * 8;
+  if (grid > need) grid = need;
+  const dim3 block(TL::WN * TL::WM * 64);
+  if constexpr (EPI == EPI_RESID) {   // microbenchmark ablations (tools/gemm_bench, dbg bits)
+    switch (a.dbg) {
+      case 0: break;
+      case 1: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 1>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 2: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 2>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 3: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 3>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 4: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 4>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 6: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 6>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 8: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 8>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 12: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 12>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 13: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 13>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 9: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 27>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      case 5: hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false, 25>), dim3(grid), block, 0, st, a); return hipGetLastError();
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (a.rowscale) hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, true>), dim3(grid), block, 0, st, a);
+  else hipLaunchKernelGGL((gemm_r3_kernel<TL, EPI, false>), dim3(grid), block, 0, st, a);
+  return hipGetLastError();
+}
+
+template <class TL>
+hipError_t launch_r3_epi(const GemmArgs& a, int epi, hipStream_t st) {
+  if (!a.W || a.a_bf16 || a.c_bf16 || a.rpg || a.k_split || a.a_plane || a.M <= 0 || a.N % TL::BN || a.N > TL::NB ||
+      a.K % 32 || a.lda % 4 || a.ldc % 4 || (a.c_plane && (a.c_plane % 8 || (epi != EPI_SWIGLU && epi != EPI_GLU))) ||
+      a.c2_plane % 8)
+    return hipErrorInvalidValue;
+  constexpr bool pairable = (TL::BN / TL::WN / 32) % 2 == 0;    // g/u 32-row blocks in one wave tile
+  switch (epi) {
+    case EPI_STORE: return launch_r3<TL, EPI_STORE>(a, st);
+    case EPI_RESID: return launch_r3<TL, EPI_RESID>(a, st);
+    case EPI_SWIGLU: if constexpr (pairable) return launch_r3<TL, EPI_SWIGLU>(a, st); else return hipErrorInvalidValue;
+    case EPI_GLU: if constexpr (pairable) return launch_r3<TL, EPI_GLU>(a, st); else return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
 int num_cus_t() {
   static int n = 0;
   if (!n) {
@@ -1376,6 +1667,24 @@ hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     case 9: return launch_x3_epi<XT<64, 32, 2, 1, 4, 2>>(a, epi, st);     // 8 waves, 128 KiB
     case 10: return launch_x3_epi<XT<32, 64, 1, 2, 4, 2>>(a, epi, st);    // 8 waves, 112 KiB
     case 11: return launch_x3_epi<XT<64, 32, 2, 1, 2, 3>>(a, epi, st);    // 4 waves, 96 KiB
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// fp32-by-split, fp32 W and X through a K-tile ring (gemm_r3_kernel).  RT<BN, BM, WN, WM, R, NB>:
+// tile BN W rows x BM X rows, WN x WM waves, R K-tiles of (BN + BM) x 128 B, bias for N <= NB.
+hipError_t gemm_r3(const GemmArgs& a, int epi, int variant, hipStream_t st) {
+  switch (variant) {
+    case 0: return launch_r3_epi<RT<256, 128, 4, 2, 3, kBiasMax>>(a, epi, st);   // 8 waves, 156 KiB
+    case 1: return launch_r3_epi<RT<128, 128, 2, 4, 4, kBiasMax>>(a, epi, st);   // 8 waves, 140 KiB
+    case 2: return launch_r3_epi<RT<64, 64, 2, 2, 6, 1536>>(a, epi, st);         // 4 waves, 102 KiB
+    case 3: return launch_r3_epi<RT<64, 32, 2, 1, 6, 1536>>(a, epi, st);         // 2 waves, 78 KiB
+    case 4: return launch_r3_epi<RT<32, 64, 1, 2, 6, 1536>>(a, epi, st);         // 2 waves, 78 KiB
+    case 5: return launch_r3_epi<RT<128, 64, 2, 2, 5, 1536>>(a, epi, st);        // 4 waves, 126 KiB (paired)
+    case 6: return launch_r3_epi<RT<64, 64, 1, 2, 6, 1536>>(a, epi, st);         // 2 waves, 102 KiB (paired)
+    case 7: return launch_r3_epi<RT<128, 128, 4, 2, 4, kBiasMax>>(a, epi, st);   // 8 waves, 140 KiB
+    case 8: return launch_r3_epi<RT<256, 128, 2, 4, 3, kBiasMax>>(a, epi, st);   // 8 waves, 156 KiB
+    case 9: return launch_r3_epi<RT<64, 64, 2, 2, 4, 1536>>(a, epi, st);         // 4 waves, 70 KiB
     default: return hipErrorInvalidValue;
   }
 }

@@ -88,6 +88,8 @@ hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // the same with the K range split over nsplit workgroups (partials in a.ws, fixed-order combine; gemm.hip)
 hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
+// the same arithmetic with fp32 W and X streamed through a K-tile ring (gemm_t.hip gemm_r3_kernel); needs a.W fp32
+hipError_t gemm_r3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 
 // a3 conv2 as an implicit GEMM over all streams: A rows gathered from the channels-last
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,

@@ -253,6 +253,7 @@ int main(int argc, char** argv) {
   a.A = A; a.lda = K; a.W = W; a.C = C; a.ldc = nout; a.bias = bias; a.R = R; a.ldr = N; a.alpha = 1.f;
   a.M = M; a.N = N; a.K = K; a.ws = ws; a.ws_ss = ws_ss; a.ws_cap = ws_cap; a.a_bf16 = 1; a.c_bf16 = cbf;
   a.C2 = (epi == 1 || (epi == 0 && !cbf)) ? C2 : nullptr;   // the session's shadowed outputs
+  if (getenv("NOC2")) a.C2 = nullptr;                         // fp32 mode: no bf16 shadow
   a.rowscale = rowscale;
   a.inv_sqrt_k = 1.0f / sqrtf((float)K);
   hipEvent_t e0, e1;
@@ -271,10 +272,10 @@ int main(int argc, char** argv) {
     const int fl = vv < 0 ? 0 : vv / 100;
     a.order_n = fl & 1;
     a.nt_store = (fl >> 1) & 1;
-    a.dbg = (fl >> 2) & 7;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA
+    a.dbg = (fl >> 2) & 15;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA; gemm_r3: see gemm_t.hip
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
-    const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 40) || (v >= 50 && v < 90);
+    const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 50) || (v >= 50 && v < 90);
     // -2: gemm() fp32 routing with W planes, -3: without, -4: with W and A planes
     a.W3 = (vv == -2 || vv == -4 || (v >= 50 && v < 90)) ? W3 : nullptr;
     a.a_plane = (vv == -4 || (v >= 60 && v < 70)) ? (int64_t)M * K : 0;
@@ -289,7 +290,7 @@ int main(int argc, char** argv) {
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
              : (v >= 50 && nsplit > 1) ? gemm_x3_splitk(a, epi, v - 50, nsplit, 0)
              : v >= 50 ? gemm_x3(a, epi, v - 50, 0)
-             : v >= 40 ? gemm_f32t(a, epi, v - 40, 0)
+             : v >= 40 ? gemm_r3(a, epi, v - 40, 0)        // 40-49: fp32 W and X, K-tile ring
              : v >= 30 ? gemm_f32t(a, epi, v - 30, 0)
              : v >= 20 ? gemm_t(a, epi, v - 20, 0)
                        : gemm_bf16_variant(a, epi, v, nsplit, 0);
