@@ -439,7 +439,9 @@ static_assert(kC3Slab * 4 + 2 * kC3Tap * 4 + 2 * kSub2C * 4 <= 160 * 1024, "conv
 
 // 400 ms (T = 13): three workgroups per stream (5 + 5 + 3 output rows); the last one's slab window
 // is clamped to the stream's 48 input rows and its positions past row 13 are not stored.
-template <int NWV, int T>   // waves per workgroup (8: two per SIMD; 4: one per SIMD, 3 tiles each); frames
+// DBG (TONE_CONV2_DBG, ablations only): bit 0 taps not re-staged (every tap reads slot 0), bit 1 no
+// split, bit 2 no MFMA
+template <int NWV, int T, int DBG = 0>   // waves per workgroup (8: two per SIMD; 4: one per SIMD, 3 tiles each); frames
 __global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2x,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        float* __restrict__ flat) {
@@ -509,10 +511,12 @@ __global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restr
     for (int ct = 0; ct < 4; ++ct) acc[k][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int j = 0; j < kC2Taps; ++j) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier_lds_c2();                                     // tap j (and the slab) landed; slot (j+1)&1 free
-    if (j + 1 < kC2Taps) stage_tap(j + 1);
-    const float* wr = ring + (j & 1) * kC3Tap;
+    if (!(DBG & 1) || j == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds_c2();                                   // tap j (and the slab) landed; slot (j+1)&1 free
+      if (j + 1 < kC2Taps && !(DBG & 1)) stage_tap(j + 1);
+    }
+    const float* wr = ring + ((DBG & 1) ? 0 : (j & 1)) * kC3Tap;
     bf16x8 w[3][4];
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
@@ -527,14 +531,27 @@ __global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restr
         const f32x4 c = *reinterpret_cast<const f32x4*>(lds + q * 32 + (((g + 4) ^ h) << 2));
         bf16x8 x0, x1, xl;
         const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+        if constexpr ((DBG & 2) != 0) {
+          x0 = __builtin_bit_cast(bf16x8, a);
+          x1 = __builtin_bit_cast(bf16x8, c);
+          xl = x0;
+        } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const __bf16 h0 = (__bf16)x[e];
-          const float r1 = x[e] - (float)h0;
-          const __bf16 h1 = (__bf16)r1;
-          x0[e] = h0;
-          x1[e] = h1;
-          xl[e] = (__bf16)(r1 - (float)h1);
+          for (int e = 0; e < 8; ++e) {
+            const __bf16 h0 = (__bf16)x[e];
+            const float r1 = x[e] - (float)h0;
+            const __bf16 h1 = (__bf16)r1;
+            x0[e] = h0;
+            x1[e] = h1;
+            xl[e] = (__bf16)(r1 - (float)h1);
+          }
+        }
+        if constexpr ((DBG & 4) != 0) {
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct)
+            acc[k][ct][0] += __builtin_bit_cast(f32x4, x0).x + __builtin_bit_cast(f32x4, x1).y + __builtin_bit_cast(f32x4, xl).z +
+                             __builtin_bit_cast(f32x4, w[0][ct]).x + __builtin_bit_cast(f32x4, w[1][ct]).y + __builtin_bit_cast(f32x4, w[2][ct]).z;
+          continue;
         }
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
@@ -581,7 +598,21 @@ hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, 
   if (T == 13) hipLaunchKernelGGL((conv2_x3_kernel<8, 13>), dim3(3 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
   else if (T != kT) return hipErrorInvalidValue;
   else if (nwv == 4) hipLaunchKernelGGL((conv2_x3_kernel<4, kT>), dim3(2 * B), dim3(256), 0, st, xs, ws, scale, shift, fl);
-  else hipLaunchKernelGGL((conv2_x3_kernel<8, kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
+  else {
+    static const int dbg = [] {   // TONE_CONV2_DBG (ablations only)
+      const char* e = std::getenv("TONE_CONV2_DBG");
+      return e ? std::atoi(e) : 0;
+    }();
+    switch (dbg) {
+      case 1: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 1>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
+      case 2: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 2>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
+      case 3: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 3>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
+      case 4: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 4>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
+      case 5: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 5>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
+      case 7: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 7>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
+      default: hipLaunchKernelGGL((conv2_x3_kernel<8, kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
+    }
+  }
   return hipGetLastError();
 }
 

@@ -1258,7 +1258,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_r3_kernel(GemmArgs 
     m0 = (t / ntn) * BM;
     n0 = (t % ntn) * BN;
   };
-  // per-lane source rows of this wave's pieces: W rows for pieces < BN / 8, X rows after
+  // per-lane source rows of this wave's pieces: W rows for pieces < BN / 8, X rows after (piece i of
+  // every wave is a W piece iff i * NW < BN / 8: compile-time, so the issue is branch-free)
+  static_assert((BN / 8) % NW == 0, "W / X pieces split at a wave boundary");
   auto issue = [&](int u) {
     if constexpr (DBG & 4) return;
     int m0, n0;
@@ -1270,10 +1272,11 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_r3_kernel(GemmArgs 
       const int pc = wid + i * NW;                               // wave-uniform
       const int r = pc * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);
-      const bool isw = pc < BN / 8;
-      const float* src = isw ? W + (int64_t)(n0 + r) * p.K : X + (int64_t)min(m0 + r - BN, p.M - 1) * p.lda;
+      const float* src;
+      if (i * NW < BN / 8) src = W + (int64_t)(n0 + r) * p.K + k0 + 4 * c;   // folds after unrolling
+      else src = X + (int64_t)min(m0 + r - BN, p.M - 1) * p.lda + k0 + 4 * c;
 #if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src + k0 + 4 * c, base + pc * 256, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, base + pc * 256, 16, 0, 0);
 #else
       (void)src;
       (void)base;
@@ -1389,21 +1392,26 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_r3_kernel(GemmArgs 
   for (int t = 0; t < G; ++t) {
     const int slot = t % R;
     // phase A: MFMA (t, h0) || read + split (t, h1)
+    __builtin_amdgcn_sched_barrier(0);
     ss += read_split(slot, 1, nxt);
     mfma(cur);
     interleave();
+    __builtin_amdgcn_sched_barrier(0);
     cur = nxt;
     // K-tile t + 1 landed: R - 2 later K-tiles stay in flight (clamped DMAs included)
     wait_vm_n<(R - 2) * IPW>();
     barrier_lds();                                               // every wave past its reads of K-tile t
     issue(min(t + R, G - 1));                                    // into slot t % R
+    __builtin_amdgcn_sched_barrier(0);
     // phase B: MFMA (t, h1) || read + split (t + 1, h0)
     const int tn = min(t + 1, G - 1);
     const bool last = (t % nk == nk - 1);                        // K-tile t ends a tile: t + 1 starts the next
     const float cn = read_split(tn % R, 0, nxt);
-    if (last) ss_next = cn; else ss += cn;
     mfma(cur);
     interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    ss_next = last ? cn : ss_next;
+    ss += last ? 0.f : cn;
     cur = nxt;
     if (last) {
       int m0, n0;
