@@ -62,6 +62,49 @@ def family_flops_per_stream(T: int = C.CHUNK_FRAMES) -> dict:
     return f
 
 
+def family_bytes_per_stream(T: int = C.CHUNK_FRAMES, precision: str = "fp32") -> dict:
+    """Algorithmic HBM bytes per stream-chunk of each GEMM family as the session runs it: A read + W read
+    (amortised over the batch: added by the caller) + C write, + the residual read/write and the bf16
+    shadow for RESID outputs.  Element sizes follow the precision: fp32 mode reads fp32 activations; bf16
+    mode bf16 activation shadows, bf16 FFN hidden and q/k/v; fp8 mode e4m3 (+1/32 scale) for the FFN and
+    q/k/v operands."""
+    d, ff = C.D_MODEL, C.D_FF
+    tr = (T + 1 - 3) // 2 + 1
+    lp = precision in ("bf16", "fp8")
+    ea = 2 if lp else 4                                   # activation operand
+    e8 = 1 + 1 / 32 if precision == "fp8" else ea         # MX operand (FFN, q/k/v in fp8 mode)
+    eh = 1 + 1 / 32 if precision == "fp8" else ea         # FFN hidden h
+    sh = 2 if lp else 0                                   # bf16 shadow of an fp32 residual output
+    f = {k: 0.0 for k in GEMM_FAMILIES}
+    for l in range(C.N_LAYERS):
+        t = tr if C.REDUCTION_POS < l <= C.UPSAMPLE_POS else T
+        s = C.mhsa_cache_rows(l)
+        f["gemm_ffn_up"] += 2 * t * (d * e8 + ff * eh)
+        f["gemm_ffn_down"] += 2 * t * (ff * eh + d * (8 + sh))
+        if l < C.MHSA_STATELESS:
+            f["gemm_qkv"] += t * d * (e8 + (3 if C.RECOMPUTE_SCORES[l] else 1) * ea)
+        else:
+            f["gemm_qkv"] += t * d * (e8 + ea) + (s + t) * d * (e8 + 2 * ea)
+        f["gemm_attn_out"] += t * d * (ea + 8 + sh)
+        f["gemm_pw1"] += t * d * (ea + 4)
+        f["gemm_pw2"] += t * d * (ea + 8 + sh)
+    f["gemm_sub_out"] = T * (C.SUB_OUT_IN * ea + d * 4)
+    f["gemm_reduce"] = tr * (4 * d * ea + d * (4 + sh))
+    return f
+
+
+def family_weight_bytes(precision: str = "fp32") -> dict:
+    """Weight bytes each GEMM family reads per step (every launch reads its W once)."""
+    d, ff = C.D_MODEL, C.D_FF
+    ew = 2 if precision in ("bf16", "fp8") else 4
+    e8 = 1 + 1 / 32 if precision == "fp8" else ew
+    nl = C.N_LAYERS
+    qkv = sum((3 * d * d if C.RECOMPUTE_SCORES[l] else d * d) if l < C.MHSA_STATELESS else 3 * d * d for l in range(nl))
+    return {"gemm_ffn_up": nl * 2 * 2 * ff * d * e8, "gemm_ffn_down": nl * 2 * ff * d * e8, "gemm_qkv": qkv * e8,
+            "gemm_attn_out": nl * d * d * ew, "gemm_pw1": nl * 2 * d * d * ew, "gemm_pw2": nl * d * d * ew,
+            "gemm_sub_out": C.SUB_OUT_IN * d * ew, "gemm_reduce": 4 * d * d * ew}
+
+
 def measured_traffic(family: str, precision: str, batch: int):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
     (scripts/pmc_traffic.sh + scripts/traffic_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950
@@ -236,6 +279,19 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
         traffic, tsrc = measured_traffic(dom, precision, B) if chunk == 2400 else (None, None)
         gemm_us = sum(v["avg_us"] * v["launches_per_step"] for v in fams.values())
         gemm_flop = sum(per_stream.values()) * B
+        # per-family roofline: the larger of the MFMA floor (algorithmic FLOP / dense peak of the dtype)
+        # and the HBM floor (algorithmic bytes / 8 TB/s) is the family's bound; frac = that floor / time
+        pb, wb = family_bytes_per_stream(fr, precision), family_weight_bytes(precision)
+        fam_roof, floor_sum = {}, 0.0
+        for k, v in fams.items():
+            us = v["avg_us"] * v["launches_per_step"]
+            t_mfma = per_stream[k] * B / (peak * 1e12) * 1e6
+            t_hbm = (pb[k] * B + wb[k]) / (HBM_PEAK_GBS * 1e9) * 1e6
+            bnd = "mfma" if t_mfma >= t_hbm else "hbm"
+            fl = max(t_mfma, t_hbm)
+            floor_sum += fl
+            fam_roof[k] = {"us_per_step": round(us, 1), "bound": bnd, "floor_us": round(fl, 1),
+                           "frac": round(fl / us, 3), "gb_per_step": round((pb[k] * B + wb[k]) / 1e9, 4)}
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": tsrc, "algo_bytes": int(algo_bytes(dom, precision, B)) if chunk == 2400 else None,
@@ -245,7 +301,9 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
                 "encoder_gemm_frac": round(gemm_flop / (gemm_us * 1e-6) / 1e12 / peak, 4),
                 "step_io_gbs": round(B * (C.IO_BYTES_PER_CHUNK + 4 * (chunk - 2400) + 4 * (fr - 10) * 35)
                                      / (elapsed / args.steps) / 1e9, 1),
-                "families_us_per_step": {k: round(v["avg_us"] * v["launches_per_step"], 1) for k, v in fams.items()}}
+                "families_us_per_step": {k: round(v["avg_us"] * v["launches_per_step"], 1) for k, v in fams.items()},
+                "gemm_families": fam_roof,
+                "gemm_roofline_frac": round(floor_sum / gemm_us, 4)}
         if precision == "fp32":
             roof["gemm_arith"] = ("fp32 as exact 3-way bf16 splits, 6 products per multiply-add on "
                                   "v_mfma_f32_32x32x16_bf16 (fp32-accurate; tests/test_gpu_parity.py)")
