@@ -616,6 +616,230 @@ hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// a3 conv2 in fp32 (split) mode, input split once per kernel row ("p3").  conv2_x3 above splits every
+// slab fragment again for each of the 121 taps (21x redundant VALU, profiles/r02_conv2_x3_ablate.txt:
+// the split costs ~58 us of 283 at B = 256).  Here the loop runs kernel row kt outer, kernel column kf
+// inner: the 5 input rows that kt reads (3 r + kt for output rows r) are split ONCE into three bf16
+// planes in LDS, and the 11 taps of that row read their X fragments from the planes directly (three
+// ds_read_b128, no VALU).  Per workgroup (stream, part of 5 output rows), 8 waves:
+//   * W taps (pre-split, natural channel order) stream through a 3-slot ring, issued by waves 0-3
+//     (3 x 1 KiB each), two taps ahead: one counted wait + one barrier per tap;
+//   * the fp32 rows of kernel row kt + 1 are fetched by waves 4-7 into an fp32 staging area (28 KiB)
+//     during the taps of kt, and split into the idle plane buffer by all waves at tap kf = 3;
+//   * 16-byte chunk swizzle g ^ s((row >> 2) & 3), s(q) = q ^ ((q & 1) << 1), on 64-byte rows (channel
+//     rows of W, position rows of X): the four 16-lane groups of a ds_read_b128 hit distinct banks for
+//     16 aligned rows.
+// Arithmetic: the six products of gemm_x3 (fp32-accurate), D[channel][position] on 16x16x32 MFMA.
+constexpr int kP3Rows = 5;                                        // output rows per workgroup
+constexpr int kP3Plane = kP3Rows * kSub1F * kSub1C;               // bf16 of one plane (5 rows x 44 x 32)
+constexpr int kP3Stage = kP3Rows * kSub1F * kSub1C;               // fp32 staged per kernel row (7040)
+constexpr int kP3StagePieces = (kP3Stage * 4 + 1023) / 1024;      // 28
+constexpr int kP3Tap = 3 * kSub2C * kSub1C;                       // bf16 of one tap (12 KiB)
+constexpr int kP3LdsBytes = 2 * 3 * kP3Plane * 2 + 3 * kP3Tap * 2 + kP3StagePieces * 1024 + 2 * kSub2C * 4;
+static_assert(kP3LdsBytes <= 160 * 1024, "conv2_p3 LDS");
+static_assert(kP3StagePieces % 4 == 0, "staging pieces over waves 4-7");
+
+__host__ __device__ __forceinline__ int p3_swz(int row) {   // 16-byte chunk XOR for 64-byte rows
+  const int q = (row >> 2) & 3;
+  return q ^ ((q & 1) << 1);
+}
+
+template <int T>
+__global__ void __launch_bounds__(512) conv2_p3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2p,
+                                                     const float* __restrict__ scale, const float* __restrict__ shift,
+                                                     float* __restrict__ flat) {
+  constexpr int NWV = 8;
+  constexpr int kParts = (T + kP3Rows - 1) / kP3Rows;
+  constexpr int kIn = (T == make_geom(3200).T ? make_geom(3200) : make_geom(2400)).sub2In;   // input rows per stream
+  constexpr int kC2PosT = T * kSub2F;
+  constexpr int kTiles = (kP3Rows * kSub2F + 15) / 16;            // 11
+  constexpr int KT = (kTiles + NWV - 1) / NWV, KU = kTiles / NWV; // position tiles per wave: max, unconditional
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kP3LdsBytes];
+  uint16_t* xpl = reinterpret_cast<uint16_t*>(lds);                               // [2][3][5][44][32] bf16
+  uint16_t* ring = xpl + 2 * 3 * kP3Plane;                                         // [3][3][64][32] bf16
+  float* stg = reinterpret_cast<float*>(ring + 3 * kP3Tap);                        // [5][44][32] fp32
+  float* sc = stg + kP3StagePieces * 256;
+  float* sh = sc + kSub2C;
+  const int b = blockIdx.x / kParts, part = blockIdx.x % kParts;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rows = min(kP3Rows, T - part * kP3Rows), posT = rows * kSub2F;
+  const float* xb = x2 + (int64_t)b * kIn * kSub1F * kSub1C;
+  if (tid < kSub2C) {
+    sc[tid] = scale[tid];
+    sh[tid] = shift[tid];
+  }
+  __syncthreads();                                                // before any LDS-DMA is in flight
+
+  // waves 0-3: tap j (clamped to the last) into ring slot j % 3, 3 pieces each
+  auto stage_tap = [&](int j) {
+    j = min(j, kC2Taps - 1);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int pc = wid * 3 + i;
+      const uint16_t* src = w2p + (int64_t)j * kP3Tap + pc * 512 + lane * 8;
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, ring + (j % 3) * kP3Tap + pc * 512, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+  // waves 4-7: the fp32 input rows 3 r + kt (r < 5, row past the stream clamped) into the staging area
+  auto stage_rows = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < kP3StagePieces / 4; ++i) {
+      const int pc = (wid - 4) + 4 * i;
+      const int e = min(pc * 256 + lane * 4, kP3Stage - 4);       // staged float index
+      const int rr = e / (kSub1F * kSub1C), o = e - rr * (kSub1F * kSub1C);
+      const int row = min(kSub2Stride * (part * kP3Rows + rr) + kt, kIn - 1);
+      const float* src = xb + (int64_t)row * kSub1F * kSub1C + o;
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, stg + pc * 256, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+  // all waves: staging -> the three planes of buffer `buf` (each thread a few 4-channel groups)
+  auto split_rows = [&](int buf) {
+    uint16_t* dst = xpl + buf * 3 * kP3Plane;
+    for (int i = tid; i < kP3Stage / 4; i += NWV * 64) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(stg + 4 * i);
+      const int pos = (4 * i) / kSub1C, ch = (4 * i) % kSub1C;   // pos = r * 44 + f
+      const int f = pos % kSub1F;
+      const int off = pos * kSub1C + ((((ch >> 3) ^ p3_swz(f)) << 3) | (ch & 4));
+      uint32_t w[3][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float t0[2], t1[2], t2[2];
+        split3_f(v[2 * h], t0[0], t1[0], t2[0]);
+        split3_f(v[2 * h + 1], t0[1], t1[1], t2[1]);
+        w[0][h] = (__float_as_uint(t0[0]) >> 16) | (__float_as_uint(t0[1]) & 0xffff0000u);
+        w[1][h] = (__float_as_uint(t1[0]) >> 16) | (__float_as_uint(t1[1]) & 0xffff0000u);
+        w[2][h] = (__float_as_uint(t2[0]) >> 16) | (__float_as_uint(t2[1]) & 0xffff0000u);
+      }
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x2*>(dst + pl * kP3Plane + off) = u32x2{w[pl][0], w[pl][1]};
+    }
+  };
+
+  // prologue: taps 0, 1; the rows of kt = 0 staged and split into buffer 0
+  if (wid < 4) {
+    stage_tap(0);
+    stage_tap(1);
+  } else {
+    stage_rows(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier_lds_c2();
+  split_rows(0);
+
+  const int n = lane & 15, g = lane >> 4;
+  const int ntile = wid + NWV * (KT - 1) < kTiles ? KT : KT - 1;  // wave-uniform
+  int xr[KT], xf[KT];                                              // output row / column of this lane's position
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    const int p = min((wid + NWV * k) * 16 + n, posT - 1);
+    xr[k] = p / kSub2F;
+    xf[k] = p % kSub2F;
+  }
+  int wofs[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int c = 16 * ct + n;
+    wofs[ct] = c * kSub1C + ((g ^ p3_swz(c)) << 3);
+  }
+  f32x4 acc[KT][4];
+#pragma unroll
+  for (int k = 0; k < KT; ++k)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[k][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt < kSub2Kt; ++kt) {
+    const uint16_t* xp = xpl + (kt & 1) * 3 * kP3Plane;
+    for (int kf = 0; kf < kSub2Kf; ++kf) {
+      const int j = kt * kSub2Kf + kf;
+      if (wid < 4) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // tap j landed, tap j + 1 in flight
+      else if (kf == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // rows of kt + 1 staged
+      barrier_lds_c2();                                           // ... for every wave; slot (j + 2) % 3 free
+      if (wid < 4) stage_tap(j + 2);
+      else if (kf == 0 && kt + 1 < kSub2Kt) stage_rows(kt + 1);  // staging free: its split was at kt - 1, kf 3
+      if (kf == 3 && kt + 1 < kSub2Kt) split_rows((kt + 1) & 1); // that buffer was last read in kt - 1
+      const uint16_t* wr = ring + (j % 3) * kP3Tap;
+      bf16x8 w[3][4];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) w[pl][ct] = *reinterpret_cast<const bf16x8*>(wr + pl * kSub2C * kSub1C + wofs[ct]);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        if (k < KU || k < ntile) {
+          const int f = xf[k] + kf;
+          const int off = (xr[k] * kSub1F + f) * kSub1C + ((g ^ p3_swz(f)) << 3);
+          const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(xp + off);
+          const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(xp + kP3Plane + off);
+          const bf16x8 x2v = *reinterpret_cast<const bf16x8*>(xp + 2 * kP3Plane + off);
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) {
+            f32x4 t = acc[k][ct];
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2][ct], x0, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1][ct], x1, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], x2v, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1][ct], x0, t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], x1, t, 0, 0, 0);
+            acc[k][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], x0, t, 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");               // the clamped tap DMAs
+  // epilogue: D[channel][position]; lane: position tile 16 + n, channels 16 ct + 4 g + r
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    if (k >= ntile) break;
+    const int p = (wid + NWV * k) * 16 + n;
+    if (p >= posT) continue;
+    float* dst = flat + ((int64_t)b * kC2PosT + part * kP3Rows * kSub2F + p) * kSub2C;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int ch = 16 * ct + 4 * g;
+      float4 y;
+      y.x = silu_f(fmaf(acc[k][ct][0], sc[ch], sh[ch]));
+      y.y = silu_f(fmaf(acc[k][ct][1], sc[ch + 1], sh[ch + 1]));
+      y.z = silu_f(fmaf(acc[k][ct][2], sc[ch + 2], sh[ch + 2]));
+      y.w = silu_f(fmaf(acc[k][ct][3], sc[ch + 3], sh[ch + 3]));
+      *reinterpret_cast<float4*>(dst + ch) = y;
+    }
+  }
+}
+
+hipError_t launch_conv2_p3(const void* x2, const void* w2p, const float* scale, const float* shift, void* flat, int B,
+                           int T, hipStream_t st) {
+  const float* xs = static_cast<const float*>(x2);
+  const uint16_t* ws = static_cast<const uint16_t*>(w2p);
+  float* fl = static_cast<float*>(flat);
+  if (T == 13) hipLaunchKernelGGL((conv2_p3_kernel<13>), dim3(3 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
+  else if (T == kT) hipLaunchKernelGGL((conv2_p3_kernel<kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// Host-side layout of w2p: [tap][plane][c 64][32 bf16], natural channel order, 16-byte chunk g of row c
+// stored at g ^ p3_swz(c).  planes[pl][c][tap][ci] are the three bf16 split terms.
+void conv2_p3_pack(const uint16_t* planes, uint16_t* w2p) {
+  for (int tap = 0; tap < kC2Taps; ++tap)
+    for (int pl = 0; pl < 3; ++pl)
+      for (int c = 0; c < kSub2C; ++c)
+        for (int ci = 0; ci < kSub1C; ++ci)
+          w2p[(((int64_t)tap * 3 + pl) * kSub2C + c) * kSub1C + (((ci >> 3) ^ p3_swz(c)) << 3) + (ci & 7)] =
+              planes[(((int64_t)pl * kSub2C + c) * kC2Taps + tap) * kSub1C + ci];
+}
+
 // Host-side layout of w2x: [tap][plane][c 64][32 bf16], the k order of a row permuted (k' = 8g + e
 // holds input channel 4g + e for e < 4, 16 + 4g + e - 4 otherwise) and its 16-byte slots swizzled
 // (slot g stored at g ^ c2_swz(c)).  planes[pl][c][tap][ci] are the three bf16 split terms.

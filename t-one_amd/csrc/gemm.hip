@@ -35,6 +35,8 @@
 #include <cstdlib>
 #include "kernels.h"
 
+#include <string>
+
 #include <type_traits>
 
 namespace tone {
@@ -1106,11 +1108,18 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
 }
 
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st, const void* w2x, int chunk) {
+                      bool bf16, hipStream_t st, const void* w2x, int chunk, const void* w2p) {
   const Geom geo = make_geom(chunk);
   // per-stream LDS slab kernel (frontend.hip): the 300 ms slab (38 rows, 107 KB) fits, 400 ms (48) does not
   if (bf16 && geo.T == kT) return launch_conv2_bf16(x2, w, scale, shift, flat, B, st);
-  if (w2x) return launch_conv2_x3(x2, w2x, scale, shift, flat, B, geo.T, st);    // fp32 split mode (frontend.hip)
+  // fp32 split mode (frontend.hip): input rows split once per kernel row (conv2_p3); TONE_CONV2_KERNEL=x3
+  // selects the per-tap split kernel (A/B measurements)
+  static const bool use_x3 = [] {
+    const char* e = std::getenv("TONE_CONV2_KERNEL");
+    return e && std::string(e) == "x3";
+  }();
+  if (w2p && !use_x3) return launch_conv2_p3(x2, w2p, scale, shift, flat, B, geo.T, st);
+  if (w2x) return launch_conv2_x3(x2, w2x, scale, shift, flat, B, geo.T, st);
   GemmArgs a{};
   a.A = x2;
   a.W = w;

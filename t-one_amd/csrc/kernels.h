@@ -95,7 +95,7 @@ hipError_t gemm_r3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,
 // epilogue SiLU(acc*scale + shift) -> flat [B*10][34*64] (f-major, channel-minor).
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st, const void* w2x = nullptr, int chunk = kChunk);
+                      bool bf16, hipStream_t st, const void* w2x = nullptr, int chunk = kChunk, const void* w2p = nullptr);
 
 // a3 conv2 in bf16 mode, one workgroup per stream over an LDS-resident input slab (frontend.hip);
 // x2 bf16 [B][38][44][32], w2c bf16 [64][3904] tap-major, flat bf16 [B*10][34*64]
@@ -107,6 +107,11 @@ hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, 
                            int T, hipStream_t st);
 // host: pack the split planes [3][64][121][32] (bf16 bits) into the conv2_x3 tap-major layout
 void conv2_x3_pack(const uint16_t* planes, uint16_t* w2x);
+// a3 conv2 in fp32 (split) mode, input rows split once per kernel row (frontend.hip conv2_p3_kernel);
+// w2p from conv2_p3_pack
+hipError_t launch_conv2_p3(const void* x2, const void* w2p, const float* scale, const float* shift, void* flat, int B,
+                           int T, hipStream_t st);
+void conv2_p3_pack(const uint16_t* planes, uint16_t* w2p);
 
 // a2 log-mel on the fp32 MFMA: power spectrum GEMM over overlapping windows, then filterbank GEMM
 // with the log / fp16 epilogue.  wave [B][2480] fp32 (from launch_mel_prep).

@@ -94,6 +94,7 @@ struct tone_session {
   void* w1t = nullptr;   // bf16 mode: conv1 weights [kt 11][c 32][kf 32] (kf >= 21 zero)
   void* w2c;
   uint16_t* w2x = nullptr;   // fp32 (split) mode: conv2 split planes packed for conv2_x3 (frontend.hip)
+  uint16_t* w2p = nullptr;   // ... and for conv2_p3 (natural channel order)
   void* wsub_out;
   float *wred, *bred, *bred_pw;
   void* wred_pw;
@@ -460,7 +461,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   if (s->debug_stop == 0) return TONE_OK;
   LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B, geo.chunk,
                              st));
-  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, s->w2x, geo.chunk));
+  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, s->w2x, geo.chunk, s->w2p));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * geo.T, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
   LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st));
@@ -678,6 +679,9 @@ int finalize_weights(tone_session* s) {
       conv2_x3_pack(pl.data(), px.data());
       CALL(dalloc(s, &s->w2x, px.size()));
       HIP_TRY(hipMemcpy(s->w2x, px.data(), px.size() * 2, hipMemcpyHostToDevice));
+      conv2_p3_pack(pl.data(), px.data());
+      CALL(dalloc(s, &s->w2p, px.size()));
+      HIP_TRY(hipMemcpy(s->w2p, px.data(), px.size() * 2, hipMemcpyHostToDevice));
     }
     CALL(upload(s, &s->scale2, sc));
     CALL(upload(s, &s->shift2, sh));
