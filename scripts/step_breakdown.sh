@@ -11,5 +11,6 @@ prof() {  # tag, bench args...
     python bench.py --steps 5 --warmup 2 --cpu-baseline-s 0 --alt 0 --config4 0 --config5 0 "$@" > gpurun_out/st_$tag.log 2>&1
   python scripts/step_trace.py "$(find /tmp/st_$tag -name '*kernel_trace.csv' | head -1)" > gpurun_out/step_$tag.txt
 }
+if [ $# -gt 0 ]; then prof "$@"; exit 0; fi   # one custom leg: tag, bench args...
 prof fp32_b256
 prof bf16_b2048 --precision bf16 --batch 2048

@@ -119,7 +119,9 @@ constexpr int kMxKB = kDff / 32;   // largest K / 32 (FFN down: 48 scale bytes p
 // kernels' slot ^= (r >> 1) & 7 makes both ds_read_b128 conflict-free
 __device__ __forceinline__ int mx_swz(int r) { return (r >> 1) & 7; }
 
-template <int BNW, int EPI, bool RS>
+// DBG (microbenchmark ablations only): bit 0 no epilogue, bit 1 side data (scales, bias, row factors)
+// loaded for the first tile only, bit 2 no MFMA; every accumulator stays live
+template <int BNW, int EPI, bool RS, int DBG = 0>
 __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   constexpr int BK = 128, QB = 128 * BK, NQW = BNW / 128, STG = (NQW + 2) * QB;
   constexpr int TI = BNW / 32, TH = TI / 2;                  // n-tiles per wave, per phase half
@@ -310,7 +312,8 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
     for (int i = 0; i < TH; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
+        acc[i][j] = (DBG & 4) ? acc[i][j] + (float)(wa[i][0] ^ xf[j][1] ^ wsa[i] ^ xs[j])
+                              : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
     // phase 1: the second half of the W tiles (the stage's last reads)
 #pragma unroll
     for (int i = 0; i < TH; ++i) {
@@ -322,7 +325,8 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
     for (int i = 0; i < TH; ++i)
 #pragma unroll
       for (int j = 2; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
+        acc[i][j] = (DBG & 4) ? acc[i][j] + (float)(wa[i][2] ^ xf[j][3] ^ wsa[i] ^ xs[j])
+                              : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
     barrier_lds();                                              // every wave's reads of stage buf done
     // phase 2
     if (t + 2 < G) issue_kt(t + 2, 0, (QPT / 2 + 1) / 2);
@@ -330,14 +334,16 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
     for (int i = 0; i < TH; ++i)
 #pragma unroll
       for (int j = 2; j < 4; ++j)
-        acc[TH + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
+        acc[TH + i][j] = (DBG & 4) ? acc[TH + i][j] + (float)(wb[i][4] ^ xf[j][5] ^ wsb[i] ^ xs[j])
+                                   : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
     // phase 3
     if (t + 2 < G) issue_kt(t + 2, (QPT / 2 + 1) / 2, QPT / 2);
 #pragma unroll
     for (int i = 0; i < TH; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[TH + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
+        acc[TH + i][j] = (DBG & 4) ? acc[TH + i][j] + (float)(wb[i][6] ^ xf[j][7] ^ wsb[i] ^ xs[j])
+                                   : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
     // K-tile t+1 landed; the first half of K-tile t+2's quarters (2 pieces each) stays in flight
     if (t + 2 < G) {
       if constexpr (QPT / 2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -347,9 +353,17 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
     }
     barrier_lds();
     if (kt == nk - 1) {
-      epilogue(t);
+      if constexpr ((DBG & 1) != 0) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)   // never true (alpha is finite): keeps every accumulator live
+            if (p.alpha == -1.2345e30f) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + 4 * (64 * (i * 4 + j) + lane)) = acc[i][j];
+      } else {
+        epilogue(t);
+      }
       zero();
-      if (t + 1 < G) {
+      if (t + 1 < G && !(DBG & 2)) {
         __syncthreads();                                        // every epilogue done with the side data
         load_side(t + 1);
         __syncthreads();
@@ -364,6 +378,17 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
   int grid = 256;
   const int need = ((ntiles + 7) / 8) * 8;
   if (grid > need) grid = need;
+  if constexpr (EPI == EPI_SWIGLU) {   // microbenchmark ablations (tools/gemm_bench MXDBG)
+    switch (a.dbg) {
+      case 0: break;
+      case 1: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 1>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 2: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 2>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 3: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 3>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 4: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 4>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 7: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 7>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (a.rs_inv) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false>), dim3(grid), dim3(512), 0, st, a);
   return hipGetLastError();

@@ -23,6 +23,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace tone {
@@ -917,7 +918,9 @@ __device__ __forceinline__ void split3(const f32x4 a, const f32x4 b, bf16x8& h, 
 
 // XS: X arrives pre-split (3 bf16 planes written by its producer, GemmArgs::a_plane) and is staged
 // like W -- no split VALU in the loop; otherwise X is fp32 and split from its LDS fragment.
-template <class TL, int EPI, bool RS, bool XS>
+// HL: only the upper half of the waves (wid >= NW / 2) issues the LDS-DMA, twice the pieces each, so each
+// SIMD pairs a wave stalled in DMA issue with one that keeps its MFMAs going.
+template <class TL, int EPI, bool RS, bool XS, bool HL = false>
 __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(GemmArgs p) {
   constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, WK = TL::WK, S = TL::S;
   constexpr int NW = WN * WM * WK, NT = NW * 64;
@@ -927,8 +930,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   constexpr int GROUP = 3 * WPL + (XS ? 3 * XPL : BMX * 32);    // floats of one wave group's slice
   constexpr int STAGE = WK * GROUP;
   constexpr int WPC = 3 * BNW / 16, XPC = XS ? 3 * BMX / 16 : BMX / 8;   // 1 KiB DMA pieces per group
-  constexpr int PIECES = WK * (WPC + XPC), IPW = PIECES / NW;
-  static_assert(PIECES % NW == 0 && IPW >= 1, "DMA pieces per wave");
+  constexpr int NL = HL ? NW / 2 : NW;                          // waves issuing the LDS-DMA
+  constexpr int PIECES = WK * (WPC + XPC), IPW = PIECES / NL;
+  static_assert(PIECES % NL == 0 && IPW >= 1, "DMA pieces per wave");
   static_assert(TI >= 1 && TJ >= 1 && WN >= TJ, "wave tile / row-scale ownership");
   static_assert(S == 2 || S == 3, "2 or 3 LDS stages");
   constexpr int RED = (WK - 1) * (NW / WK) * 64 * TI * TJ * 16;  // K-split partials (floats)
@@ -944,7 +948,15 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   const int lr = lane & 31, lh = lane >> 5;
   const int ntn = p.N / BNW;
   int m0, n0;
-  if ((ntn & 7) == 0) {
+  if (p.xcd_a) {
+    // 2D XCD blocks: XCD x owns n-tiles of group x % a and m-tiles of group x / a, so its compulsory L2
+    // fill is W / a + X / (8 / a) instead of all of W (or all of X); the launcher picks a and checks
+    // the divisibility (grid = tiles, a multiple of 8)
+    const int a = p.xcd_a, xcd = blockIdx.x & 7, li = blockIdx.x >> 3;
+    const int npg = ntn / a, mpg = ((p.M + BMX - 1) / BMX) / (8 / a);
+    n0 = ((xcd % a) * npg + li % npg) * BNW;
+    m0 = ((xcd / a) * mpg + li / npg) * BMX;
+  } else if ((ntn & 7) == 0) {
     // large W (FFN up: 7 MB of planes > one XCD's 4 MB L2): XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8)
     // for every M-tile, so each W plane row is fetched into one L2 only and the X tile is reused
     // by the XCD's N-tiles back to back
@@ -973,9 +985,10 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   auto stage = [&](int buf, int kt) {
     float* base = lds + buf * STAGE;
     (void)base;
+    if (HL && wid < NW / 2) return;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-      const int piece = wid + i * NW;                           // wave-uniform
+      const int piece = (HL ? wid - NW / 2 : wid) + i * NL;     // wave-uniform
       const int g = piece / (WPC + XPC), pr = piece % (WPC + XPC);
       const int kb = kofs + (kt * WK + g) * 32;
       const void* src;
@@ -1152,10 +1165,51 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
 }
 
+// XCD blocking for gemm_x3 (GemmArgs::xcd_a): the a in {1, 2, 4, 8} whose per-XCD compulsory fill
+// (W planes / a + X / (8 / a)) is smallest, or 0 (default order) when the tiles do not divide evenly.
+// Off unless TONE_X3_XCD=1: on FFN up at B = 256 it raises the L2 hit rate from 0.81 to 0.87 and halves
+// the fabric fetch (30 -> 18 MB) without changing the time (49.8 vs 49.2 us) -- the kernel is bound by
+// its LDS-DMA issue rate, not by L2 misses.
+template <class TL>
+int x3_xcd_split(const GemmArgs& a) {
+  static const int off = [] {
+    const char* e = std::getenv("TONE_X3_XCD");
+    return !(e && std::atoi(e) == 1);
+  }();
+  const int ntn = a.N / TL::BNW, ntm = (a.M + TL::BMX - 1) / TL::BMX;
+  if (off || a.k_split || (ntn & 7) == 0 || a.M % TL::BMX) return 0;
+  const double wb = 6.0 * a.N * a.K, xb = (a.a_plane ? 6.0 : 4.0) * a.M * a.K;
+  int best = 0;
+  double cost = wb + xb / 8;                      // the default XCD-contiguous m-major order: all of W
+  for (int s = 2; s <= 8; s *= 2) {
+    if (ntn % s || ntm % (8 / s)) continue;
+    const double c = wb / s + xb / (8 / s);
+    if (c < 0.8 * cost) { cost = c; best = s; }
+  }
+  return best;
+}
+
 template <class TL, int EPI>
-hipError_t launch_x3(const GemmArgs& a, hipStream_t st) {
+hipError_t launch_x3(const GemmArgs& a0, hipStream_t st) {
+  GemmArgs a = a0;
+  a.xcd_a = x3_xcd_split<TL>(a0);
   const dim3 tiles((a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX), a.k_split ? a.K / a.k_split : 1);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
+  // TONE_X3_HL=1: half the waves issue the LDS-DMA (A/B only: 10-40 % slower on every B = 256 shape --
+  // the fill rate scales with the number of issuing waves, tools/dma_bench.hip)
+  static const int hl = [] {
+    const char* e = std::getenv("TONE_X3_HL");
+    return e ? std::atoi(e) : 0;
+  }();
+  constexpr int kNW = TL::WN * TL::WM * TL::WK;
+  constexpr int kPieces = TL::WK * (3 * TL::BNW / 16 + TL::BMX / 8);
+  if constexpr (kNW >= 4 && kPieces % (kNW / 2) == 0) {
+    if (hl && !a.a_plane) {
+      if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, false, true>), tiles, block, 0, st, a);
+      else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, false, true>), tiles, block, 0, st, a);
+      return hipGetLastError();
+    }
+  }
   if (a.a_plane) {
     if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, true>), tiles, block, 0, st, a);
     else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, true>), tiles, block, 0, st, a);

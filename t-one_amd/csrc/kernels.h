@@ -45,6 +45,8 @@ struct GemmArgs {
   int64_t c_plane;    // STORE / SWIGLU / GLU: C written as 3 bf16 planes instead of fp32
   int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
   int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
+  int xcd_a;          // gemm_x3: XCD x owns the 2D tile block (n-group x % a, m-group x / a) of an a x (8 / a)
+                      // split (set by the launcher; 0 = the default order)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -71,6 +73,7 @@ struct MxArgs {
   uint8_t* C8s;           // ... with E8M0 scales [M][N/64]
   int64_t ldc8s;
   int M, N, K;
+  int dbg;                // microbenchmarks only (gemm_mx.hip DBG bits); 0 in the session
 };
 hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st);
 // bf16 [M][K] (ldx elements) -> e4m3 [M][K] + E8M0 [M][K/32]; inv (optional): 1/(||row||/sqrt(K) + 1e-8)

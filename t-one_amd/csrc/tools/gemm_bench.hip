@@ -145,6 +145,7 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   a.A = A8; a.lda = K; a.As = As; a.ldas = K / 32; a.W = W8; a.Ws = Ws; a.rs_inv = rowscale ? inv : nullptr;
   a.bias = bias; a.C = C; a.ldc = nout; a.c_bf16 = 0; a.R = R; a.ldr = N; a.alpha = 1.f;
   a.C8 = C8; a.C8s = C8s; a.ldc8s = nout / 32; a.M = M; a.N = N; a.K = K;
+  a.dbg = getenv("MXDBG") ? atoi(getenv("MXDBG")) : 0;   // gemm_mx.hip DBG bits (SWIGLU only)
   if (epi >= 2) a.ldc = nout;   // bytes of C8 rows
   hipError_t rc = gemm_mx(a, epi, 0);
   if (rc != hipSuccess) { printf("{\"variant\": 99, \"error\": \"%s\"}\n", hipGetErrorString(rc)); return; }
