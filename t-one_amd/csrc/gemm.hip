@@ -943,7 +943,10 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   // TONE_GEMM_P (experiments): bit 0 SwiGLU, bit 1 GLU on gemm_p; low nibble of bits 4.. = gemm_p variant
   const char* route_env = getenv("TONE_GEMM_P");
   const int route = route_env ? atoi(route_env) : 1;   // in-step A/B (scripts/ab_route.py): SwiGLU only, plain stores
-  const int pv = (route >> 4) & 15;
+  // default variant 7: 2D XCD blocks with 4 n-groups where the tiles divide evenly (87.6-90.9 vs 88-93 us at
+  // M = 20480, 166 vs 182 at 40960; profiles/r02_gemm_p_xcd.txt), else the XCD-contiguous order
+  const int pv0 = (route >> 4) & 15;
+  const int pv = (pv0 == 0 && (a.N / 256) % 4 == 0 && ((a.M + 255) / 256) % 2 == 0) ? 7 : pv0;
   if (epi == EPI_SWIGLU && (route & 1) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
   if (epi == EPI_GLU && (route & 2) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
   if (epi == EPI_SWIGLU && a.N % 256 == 0 && t256 >= 192) return gemm_t(a, epi, 0, st);

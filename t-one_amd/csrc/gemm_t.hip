@@ -358,6 +358,12 @@ __global__ void __launch_bounds__(512) gemm_p_kernel(GemmArgs p) {
   __syncthreads();                                              // no DMA in flight yet
 
   auto tile_of = [&](int u, int& m0, int& n0) {
+    if (p.xcd_a) {   // 2D XCD blocks (GemmArgs::xcd_a): XCD x owns n-group x % a and m-group x / a
+      const int a = p.xcd_a, npg = ntn / a, li = jb + (u / nk) * nxb;
+      n0 = ((xcd % a) * npg + li % npg) << 8;
+      m0 = ((xcd / a) * (ntm / (8 / a)) + li / npg) << 8;
+      return;
+    }
     const int t = tbeg + jb + (u / nk) * nxb;
     m0 = (t / ntn) << 8;
     n0 = (t % ntn) << 8;
@@ -1684,7 +1690,15 @@ hipError_t launch_p_epi(const GemmArgs& a, int epi, hipStream_t st) {
 
 // variant 0: gemm_p_kernel; 1: the same with static priority for waves 4-7; 2 / 3: paired epilogues with
 // non-temporal / sc1 (write-through, L2-dropping) 16-byte stores
-hipError_t gemm_p(const GemmArgs& a, int epi, int variant, hipStream_t st) {
+hipError_t gemm_p(const GemmArgs& a0, int epi, int variant, hipStream_t st) {
+  GemmArgs a = a0;
+  if (variant >= 6 && variant <= 8) {   // 2D XCD blocks, a = 2 / 4 / 8 n-groups (tiles must divide evenly)
+    const int sa = variant == 6 ? 2 : variant == 7 ? 4 : 8;
+    const int ntn = a.N / 256, ntm = (a.M + 255) / 256;
+    if (ntn % sa || ntm % (8 / sa)) return hipErrorInvalidValue;
+    a.xcd_a = sa;
+    variant = 0;
+  }
   switch (variant) {
     case 0: return launch_p_epi<false>(a, epi, st);
     case 1: return launch_p_epi<true>(a, epi, st);
