@@ -1070,6 +1070,13 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     // step the ring kernel is slower (profiles/r02_r3_sweep.jsonl)
     if (epi == EPI_STORE && a.N == 768 && a.M >= 4096 && a.W && !a.rowscale)
       return gemm_r3(a, epi, a.M >= 8192 ? 0 : 1, st);
+    // ping-pong schedule (gemm_pp) for the FFN up-projection; TONE_PP = 1 + variant, 0 = off
+    static const int pp = [] {
+      const char* e = std::getenv("TONE_PP");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (pp > 0 && a.W3b && epi == EPI_SWIGLU && a.N % 256 == 0 && (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200)
+      return gemm_pp(a, epi, pp - 1, st);
     if (epi == EPI_SWIGLU && a.N % 256 == 0)
       return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200 ? 7 : 6, st);
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);

@@ -26,153 +26,10 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "gemm_common.h"
+
 namespace tone {
 namespace {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kBiasMax = 3072;   // largest N of the encoder (FFN up: W1|Wv)
-
-template <int BNW_, int BMX_, int WN_, int WM_>
-struct TT {
-  static constexpr int BNW = BNW_, BMX = BMX_, WN = WN_, WM = WM_;
-};
-
-__device__ __forceinline__ uint32_t pk2(float a, float b) {
-  const __bf16 ha = (__bf16)a, hb = (__bf16)b;
-  return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
-}
-
-__device__ __forceinline__ float sumsq8(bf16x8 v, float acc) {
-  const bf16x2 p0 = __builtin_shufflevector(v, v, 0, 1), p1 = __builtin_shufflevector(v, v, 2, 3);
-  const bf16x2 p2 = __builtin_shufflevector(v, v, 4, 5), p3 = __builtin_shufflevector(v, v, 6, 7);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(p0, p0, acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(p1, p1, acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(p2, p2, acc, false);
-  return __builtin_amdgcn_fdot2_f32_bf16(p3, p3, acc, false);
-}
-
-// bf16-output activations: v_exp_f32 + v_rcp_f32 (~1 ulp fp32, far below the bf16 rounding of the
-// result) instead of the IEEE expf / division sequences
-__device__ __forceinline__ float fast_sigmoid(float x) {
-  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
-}
-__device__ __forceinline__ float fast_silu(float x) { return x * fast_sigmoid(x); }
-
-__device__ __forceinline__ void barrier_lds() {   // keeps LDS-DMA in flight (no vmcnt(0) fence)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
-
-// 16 values of one 32x32 D tile for this lane (row m fixed; columns c + (r&3) + 8(r>>2) + 4h) as
-// bf16: pack to 4-element runs, swap runs between the lane halves (T21) so each lane owns 8
-// contiguous elements, and store 2 x 16 B.  rowp points at column c of row m.  All lanes must
-// execute the swaps; only the store is predicated.
-__device__ __forceinline__ void store_tile_bf16(uint16_t* rowp, const float (&v)[16], int lh, bool ok) {
-  uint32_t px[4], py[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    px[g] = pk2(v[4 * g], v[4 * g + 1]);
-    py[g] = pk2(v[4 * g + 2], v[4 * g + 3]);
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k += 2) {
-    const auto rx = __builtin_amdgcn_permlane32_swap(px[k], px[k + 1], false, false);
-    const auto ry = __builtin_amdgcn_permlane32_swap(py[k], py[k + 1], false, false);
-    const u32x4 o = {rx[0], ry[0], rx[1], ry[1]};
-    if (ok) *reinterpret_cast<u32x4*>(rowp + 8 * k + 8 * lh) = o;
-  }
-}
-
-// The same 16 values stored as their exact 3-term bf16 split into three planes `plane` apart.
-__device__ __forceinline__ void store_tile_split(uint16_t* rowp, int64_t plane, const float (&v)[16], int lh, bool ok) {
-  float t0[16], t1[16], t2[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) split3_f(v[r], t0[r], t1[r], t2[r]);
-  store_tile_bf16(rowp, t0, lh, ok);
-  store_tile_bf16(rowp + plane, t1, lh, ok);
-  store_tile_bf16(rowp + 2 * plane, t2, lh, ok);
-}
-
-// Per-tile epilogue shared by both kernels.  acc[i][j] is the wave's 32x32 D tile (n-tile i,
-// m-tile j); rd[m - m0] the row-scale denominators, sb[n - n0] the bias (both LDS).
-template <int EPI, bool RS, int TI, int TJ, int WTN, int WTM>
-__device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[TI][TJ], const float* rd, const float* sb,
-                                              int m0, int n0, int wn, int wm, int lr, int lh) {
-  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int ml = wm * WTM + 32 * j + lr, m = m0 + ml;
-    const bool ok = m < p.M;
-    const int64_t mrow = min(m, p.M - 1);
-    const float inv = RS ? 1.0f / rd[ml] : 1.0f;
-    if constexpr (PAIRED) {
-#pragma unroll
-      for (int ip = 0; ip < TI / 2; ++ip) {
-        const int nl = wn * WTN + 64 * ip;                   // g rows nl..nl+31, u rows nl+32..nl+63
-        float o[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int n = nl + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const float g = fmaf(acc[2 * ip][j][r], inv, sb[n]);
-          const float u = fmaf(acc[2 * ip + 1][j][r], inv, sb[n + 32]);
-          if (p.c_bf16) o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
-          else o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);   // fp32 output: IEEE exp/div
-        }
-        if (p.c_bf16) {
-          store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, o, lh, ok);
-        } else if (p.c_plane) {   // fp32 split mode: the next GEMM's A as 3 bf16 planes
-          store_tile_split(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, p.c_plane, o, lh, ok);
-        } else {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 w = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
-            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + (n0 + nl) / 2 + 8 * g + 4 * lh) = w;
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int nl = wn * WTN + 32 * i, nb = n0 + nl;
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = fmaf(acc[i][j][r], inv, sb[nl + (r & 3) + 8 * (r >> 2) + 4 * lh]);
-        if constexpr (EPI == EPI_RESID) {
-          f32x4 rr[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) rr[g] = *reinterpret_cast<const f32x4*>(p.R + mrow * p.ldr + nb + 8 * g + 4 * lh);
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 o;
-            o.x = rr[g].x + p.alpha * v[4 * g];
-            o.y = rr[g].y + p.alpha * v[4 * g + 1];
-            o.z = rr[g].z + p.alpha * v[4 * g + 2];
-            o.w = rr[g].w + p.alpha * v[4 * g + 3];
-            v[4 * g] = o.x; v[4 * g + 1] = o.y; v[4 * g + 2] = o.z; v[4 * g + 3] = o.w;
-            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
-          }
-          if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
-          else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);
-        } else if (p.c_bf16) {
-          store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + nb, v, lh, ok);
-        } else {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 o = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
-            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
-          }
-          if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
-          else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);   // bf16 shadow (fp32 C)
-        }
-      }
-    }
-  }
-}
 
 template <class TL, int EPI, bool RS>
 __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_t_kernel(GemmArgs p) {
@@ -907,20 +764,6 @@ struct XT {
   static constexpr int BNW = BNW_, BMX = BMX_, WN = WN_, WM = WM_, WK = WK_, S = S_;
 };
 
-// 8 fp32 values -> their three bf16 terms (round-to-nearest-even at each level)
-__device__ __forceinline__ void split3(const f32x4 a, const f32x4 b, bf16x8& h, bf16x8& m, bf16x8& l) {
-  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 x0 = (__bf16)x[e];
-    const float r1 = x[e] - (float)x0;
-    const __bf16 x1 = (__bf16)r1;
-    const float r2 = r1 - (float)x1;
-    h[e] = x0;
-    m[e] = x1;
-    l[e] = (__bf16)r2;
-  }
-}
 
 // XS: X arrives pre-split (3 bf16 planes written by its producer, GemmArgs::a_plane) and is staged
 // like W -- no split VALU in the loop; otherwise X is fp32 and split from its LDS fragment.
@@ -1168,6 +1011,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
     if (wk == 0 && wn < TJ && lh == 0) rden[wm * WTM + 32 * jss + lr] = sqrtf(t) * p.inv_sqrt_k + kRmsEps;
     barrier_lds();
   }
+  if (p.dbg & 8) return;                                        // microbenchmark: no epilogue
   if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
 }
 
@@ -1764,5 +1608,6 @@ hipError_t gemm_r3(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     default: return hipErrorInvalidValue;
   }
 }
+
 
 }  // namespace tone

@@ -45,6 +45,7 @@ struct GemmArgs {
   int64_t c_plane;    // STORE / SWIGLU / GLU: C written as 3 bf16 planes instead of fp32
   int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
   int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
+  const uint16_t* W3b; // fp32 mode: the same planes K16-blocked, [3][K/16][N][16] (gemm_pp), or nullptr
   int xcd_a;          // gemm_x3: XCD x owns the 2D tile block (n-group x % a, m-group x / a) of an a x (8 / a)
                       // split (set by the launcher; 0 = the default order)
 };
@@ -90,6 +91,9 @@ hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3
 hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // the same with the K range split over nsplit workgroups (partials in a.ws, fixed-order combine; gemm.hip)
+// the same arithmetic, ping-pong schedule (two wave groups alternating LDS/VALU and MFMA segments;
+// gemm_t.hip gemm_pp_kernel); needs a.W3b
+hipError_t gemm_pp(const GemmArgs& a, int epi, int variant, hipStream_t st);
 hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // the same arithmetic with fp32 W and X streamed through a K-tile ring (gemm_t.hip gemm_r3_kernel); needs a.W fp32
 hipError_t gemm_r3(const GemmArgs& a, int epi, int variant, hipStream_t st);

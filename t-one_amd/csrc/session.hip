@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -101,6 +102,7 @@ struct tone_session {
   float *whead, *bhead;
   LayerW L[16];
   std::map<const void*, const uint16_t*> w3;   // fp32 (split) mode: GEMM weight -> its bf16 planes
+  std::map<const void*, const uint16_t*> w3b;  // ... and their K16-blocked copy (encoder weights, gemm_pp)
 
   // activations
   float *wave, *power, *feats, *rA, *rB, *qkv, *kvp, *g, *probs;
@@ -225,7 +227,7 @@ int upload_mx(tone_session* s, MxW* out, const std::vector<float>& v, int N, int
 // GEMM weight in the session's precision (fp32, or bf16 bits).  fp32 (split) mode also uploads the
 // exact three-term bf16 split [3][N][K] (w = w0 + w1 + w2, each term the bf16 rounding of what the
 // previous ones leave) that gemm_x3 reads.
-int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
+int upload_w(tone_session* s, void** out, const std::vector<float>& v, int K = 0) {
   if (!bfmode(s)) {
     float* p;
     int rc = upload(s, &p, v);
@@ -246,6 +248,20 @@ int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
     if (rc) return rc;
     HIP_TRY(hipMemcpy(d, pl.data(), pl.size() * 2, hipMemcpyHostToDevice));
     s->w3[p] = d;
+    static const bool pp = std::getenv("TONE_PP") && std::atoi(std::getenv("TONE_PP")) > 0;
+    if (pp && K > 0 && K % 16 == 0 && n % K == 0) {   // K16-blocked copy [3][K/16][N][16] for gemm_pp (TONE_PP)
+      const size_t N = n / K;
+      std::vector<uint16_t> bl(3 * n);
+      for (int q = 0; q < 3; ++q)
+        for (int kb = 0; kb < K / 16; ++kb)
+          for (size_t r = 0; r < N; ++r)
+            std::memcpy(&bl[(((size_t)q * (K / 16) + kb) * N + r) * 16], &pl[(size_t)q * n + r * K + kb * 16], 32);
+      uint16_t* db;
+      rc = dalloc(s, &db, bl.size());
+      if (rc) return rc;
+      HIP_TRY(hipMemcpy(db, bl.data(), bl.size() * 2, hipMemcpyHostToDevice));
+      s->w3b[p] = db;
+    }
     return TONE_OK;
   }
   std::vector<uint16_t> hb(v.size());
@@ -400,6 +416,8 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   if (s->precision == TONE_PRECISION_FP32) {
     auto it = s->w3.find(W);
     a.W3 = it == s->w3.end() ? nullptr : it->second;
+    auto ib = s->w3b.find(W);
+    a.W3b = ib == s->w3b.end() ? nullptr : ib->second;
   }
   LAUNCH(fam, gemm(a, epi, bf, st));
   return TONE_OK;
@@ -725,9 +743,9 @@ int finalize_weights(tone_session* s) {
           b13[64 * q + r] = (*b1)[src];
           b13[64 * q + 32 + r] = (*bv)[src];
         }
-      CALL(upload_w(s, &lw.w13[f], w13));
+      CALL(upload_w(s, &lw.w13[f], w13, D));
       CALL(upload(s, &lw.b13[f], b13));
-      CALL(upload_w(s, &lw.w2[f], *w2));
+      CALL(upload_w(s, &lw.w2[f], *w2, kDff));
       if (s->precision == TONE_PRECISION_FP8) {
         CALL(upload_mx(s, &lw.mx13[f], w13, 2 * kDff, D));
         CALL(upload_mx(s, &lw.mx2[f], *w2, D, kDff));
@@ -768,7 +786,7 @@ int finalize_weights(tone_session* s) {
           bqkv[m * D + n] = (*bias[src])[n];
         }
       }
-      CALL(upload_w(s, &lw.wqkv, wqkv));
+      CALL(upload_w(s, &lw.wqkv, wqkv, D));
       if (s->precision == TONE_PRECISION_FP8) CALL(upload_mx(s, &lw.mxqkv, wqkv, nb * D, D));
       CALL(upload(s, &lw.bqkv, bqkv));
     } else {
@@ -777,9 +795,9 @@ int finalize_weights(tone_session* s) {
       std::memcpy(wkv.data() + (size_t)D * D, wv->data(), (size_t)D * D * 4);
       std::memcpy(bkv.data(), bk->data(), D * 4);
       std::memcpy(bkv.data() + D, bv->data(), D * 4);
-      CALL(upload_w(s, &lw.wq, *wq));
+      CALL(upload_w(s, &lw.wq, *wq, D));
       CALL(upload(s, &lw.bq, *bq));
-      CALL(upload_w(s, &lw.wkv, wkv));
+      CALL(upload_w(s, &lw.wkv, wkv, D));
       if (s->precision == TONE_PRECISION_FP8) {
         CALL(upload_mx(s, &lw.mxq, *wq, D, D));
         CALL(upload_mx(s, &lw.mxkv, wkv, 2 * D, D));
@@ -787,7 +805,7 @@ int finalize_weights(tone_session* s) {
       CALL(upload(s, &lw.bkv, bkv));
       CALL(upload(s, &lw.norm_att, *natt));
     }
-    CALL(upload_w(s, &lw.wo, *wo));
+    CALL(upload_w(s, &lw.wo, *wo, D));
     CALL(upload(s, &lw.bo, *bo));
 
     const std::string c = p + "conv.";
@@ -813,7 +831,7 @@ int finalize_weights(tone_session* s) {
         bp[64 * q + r] = (*pb1)[src];
         bp[64 * q + 32 + r] = (*pb1)[D + src];
       }
-    CALL(upload_w(s, &lw.wpw1, wp));
+    CALL(upload_w(s, &lw.wpw1, wp, D));
     CALL(upload(s, &lw.bpw1, bp));
     std::vector<float> wd((size_t)D * kConvK), bd(D);
     for (int ch = 0; ch < D; ++ch) {
@@ -823,7 +841,7 @@ int finalize_weights(tone_session* s) {
     }
     CALL(upload(s, &lw.wdw, wd));
     CALL(upload(s, &lw.bdw, bd));
-    CALL(upload_w(s, &lw.wpw2, *pw2));
+    CALL(upload_w(s, &lw.wpw2, *pw2, D));
     CALL(upload(s, &lw.bpw2, *pb2));
     CALL(upload(s, &lw.norm_out, *nout));
   }
