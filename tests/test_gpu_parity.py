@@ -382,6 +382,37 @@ def test_fp8_staggered_streams(weights, oracle):
         s.close()
 
 
+@pytest.mark.parametrize("prec,b", [("fp32", 300), ("bf16", 1000), ("fp8", 1000)])
+def test_ragged_batches(weights, oracle, prec, b):
+    """Batch sizes that are not multiples of any GEMM tile and cross the launchers' routing thresholds:
+    partial last M-tiles (M = 10 B, 5 B in the reduced block, B (S + T) for the k|v projections of layers
+    14 / 15), the fp32 ring kernel's M >= 4096 route, gemm_p / MX tiles at a non-multiple of 256.  Two
+    stateful chunks; fp32 compares every stream at the 1e-3 bar, bf16 / fp8 sampled streams (always
+    including the last one) at their measured bounds."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    s = ToneSession(weights, precision=prec, max_batch=b)
+    rng = np.random.default_rng(41)
+    pick = np.arange(b) if prec == "fp32" else np.unique(np.r_[np.arange(0, b, 50), b - 1])
+    st = np.zeros((b, C.STATE_SIZE), np.float16)
+    st_o = np.zeros((len(pick), C.STATE_SIZE), np.float16)
+    try:
+        for c in range(2):
+            pcm = synthetic_pcm(rng, b)
+            lp_g, st = gpu_step(s, pcm, st)
+            if prec == "fp32":
+                lp_o, st_ref = oracle.step(pcm, st_o)
+                assert_logp_close(lp_g, lp_o, what=f"B={b} chunk {c}")
+                assert_state_close(st, st_ref, what=f"B={b} chunk {c}")
+                st_o = st.copy()            # next oracle step from the device state: per-step error
+            else:
+                lp_o, st_o = oracle.step(pcm[pick], st_o)
+                bounds = (BF16_MAX, BF16_P99, BF16_MARGIN) if prec == "bf16" else (FP8_MAX, FP8_P99, FP8_MARGIN)
+                assert_bf16_close(lp_g[pick], lp_o, f"{prec} B={b} chunk {c}", bounds, 0.995 if prec == "bf16" else 0.99)
+    finally:
+        s.close()
+
+
 @pytest.mark.parametrize("prec", ["bf16", "fp8"])
 def test_low_precision_example_audio_greedy_decode(weights, oracle, prec):
     """Greedy decode of the reference's example utterance in bf16 / fp8 mode == the oracle decode of the
