@@ -40,7 +40,9 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <class TL, int EPI, bool RS>
+// RG: the pieces go global -> VGPR -> ds_write_b128 instead of LDS-DMA: loaded in L(j) for segment j + R - 1,
+// written in L(j + 1), read from L(j + R - 1) on (two register sets, the K loop unrolled by two; nk even).
+template <class TL, int EPI, bool RS, bool RG = false>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs p) {
   constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, KS = TL::KS, R = TL::R;
   static_assert(WN * WM == 8, "8 waves");
@@ -143,8 +145,23 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs p) {
   for (int j = 0; j < TJ; ++j) ss[j] = 0.f;
   bf16x8 w[KS][3][TI], xs[KS][3][TJ];
 
-  auto seg_load = [&](int kt) {
-    if (kt + R - 1 < nk) stage(kt + R - 1);
+  u32x4 rg0[IPW], rg1[IPW];
+  auto gload = [&](int seg, u32x4(&r)[IPW]) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) r[i] = *reinterpret_cast<const u32x4*>(src0[i] + seg * sstep[i]);
+  };
+  auto swrite = [&](int seg, const u32x4(&r)[IPW]) {
+    uint8_t* base = lds + (seg % R) * STAGE;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) *reinterpret_cast<u32x4*>(base + doff[i] + lane * 16) = r[i];
+  };
+  auto seg_load = [&](int kt, u32x4(&rw)[IPW], u32x4(&rl)[IPW]) {
+    if constexpr (RG) {
+      if (kt + R - 2 < nk) swrite(kt + R - 2, rw);
+      if (kt + R - 1 < nk) gload(kt + R - 1, rl);
+    } else {
+      if (kt + R - 1 < nk) stage(kt + R - 1);
+    }
     const uint8_t* base = lds + (kt % R) * STAGE;
     f32x4 xv[KS][TJ][2];
 #pragma unroll
@@ -187,7 +204,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs p) {
 #pragma unroll
         for (int i = 0; i < TI; ++i) asm volatile("" : "+v"(w[ks][pl][i]));
       }
-    if (!(p.dbg & 256)) wait_segs(min(kt + R, nk) - (kt + 2));   // this wave's pieces of segment kt + 1 landed
+    if (!RG && !(p.dbg & 256)) wait_segs(min(kt + R, nk) - (kt + 2));   // this wave's pieces of segment kt + 1 landed
   };
   auto seg_mfma = [&]() {
     if (no_mfma) return;
@@ -211,17 +228,37 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs p) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  const int pro = min(R - 1, nk);
-  for (int s = 0; s < pro; ++s) stage(s);
-  wait_segs(pro - 1);                                 // segment 0 landed (this wave's pieces)
-  bar();                                              // ... and every wave's; sbias visible
   const bool lock = p.dbg & 64;                       // A/B: both groups in lockstep (no ping-pong)
-  if (grp == 1 && !lock) bar();                       // group 1 runs one segment behind
-  for (int kt = 0; kt < nk; ++kt) {
-    seg_load(kt);
+  if constexpr (RG) {
+    for (int s = 0; s < R - 2 && s < nk; ++s) {
+      gload(s, rg0);
+      swrite(s, rg0);
+    }
+    if (R - 2 < nk) gload(R - 2, rg0);
     bar();
-    seg_mfma();
-    if (kt + 1 < nk || grp == 0 || lock) bar();
+    if (grp == 1 && !lock) bar();
+    for (int kt = 0; kt < nk; kt += 2) {              // nk even (launcher)
+      seg_load(kt, rg0, rg1);
+      bar();
+      seg_mfma();
+      bar();
+      seg_load(kt + 1, rg1, rg0);
+      bar();
+      seg_mfma();
+      if (kt + 2 < nk || grp == 0 || lock) bar();
+    }
+  } else {
+    const int pro = min(R - 1, nk);
+    for (int s = 0; s < pro; ++s) stage(s);
+    wait_segs(pro - 1);                               // segment 0 landed (this wave's pieces)
+    bar();                                            // ... and every wave's; sbias visible
+    if (grp == 1 && !lock) bar();                     // group 1 runs one segment behind
+    for (int kt = 0; kt < nk; ++kt) {
+      seg_load(kt, rg0, rg1);
+      bar();
+      seg_mfma();
+      if (kt + 1 < nk || grp == 0 || lock) bar();
+    }
   }
 
   float invj[TJ];
@@ -234,7 +271,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(GemmArgs p) {
   tile_epilogue_inv<EPI, RS, TI, TJ, WTN, WTM>(p, acc, invj, sbias, m0, n0, wn, wm, lr, lh);
 }
 
-template <class TL, int EPI>
+template <class TL, int EPI, bool RG = false>
 hipError_t launch_pp(const GemmArgs& a0, hipStream_t st) {
   GemmArgs a = a0;
   a.xcd_a = 0;
@@ -249,12 +286,13 @@ hipError_t launch_pp(const GemmArgs& a0, hipStream_t st) {
     }
   }
   const dim3 tiles(ntn * ntm), block(512);
-  if (a.rowscale) hipLaunchKernelGGL((gemm_pp_kernel<TL, EPI, true>), tiles, block, 0, st, a);
-  else hipLaunchKernelGGL((gemm_pp_kernel<TL, EPI, false>), tiles, block, 0, st, a);
+  if (RG && (a.K / (16 * TL::KS)) % 2) return hipErrorInvalidValue;
+  if (a.rowscale) hipLaunchKernelGGL((gemm_pp_kernel<TL, EPI, true, RG>), tiles, block, 0, st, a);
+  else hipLaunchKernelGGL((gemm_pp_kernel<TL, EPI, false, RG>), tiles, block, 0, st, a);
   return hipGetLastError();
 }
 
-template <class TL>
+template <class TL, bool RG = false>
 hipError_t launch_pp_epi(const GemmArgs& a, int epi, hipStream_t st) {
   if (!a.W3b || a.a_bf16 || a.c_bf16 || a.rpg || a.a_plane || a.k_split || a.M <= 0 || a.N % TL::BNW ||
       a.K % (16 * TL::KS) || a.K / (16 * TL::KS) < 1 || a.lda % 4 || a.ldc % 8 ||
@@ -262,10 +300,10 @@ hipError_t launch_pp_epi(const GemmArgs& a, int epi, hipStream_t st) {
     return hipErrorInvalidValue;
   constexpr bool pairable = (TL::BNW / TL::WN / 32) % 2 == 0;
   switch (epi) {
-    case EPI_STORE: return launch_pp<TL, EPI_STORE>(a, st);
-    case EPI_RESID: return launch_pp<TL, EPI_RESID>(a, st);
-    case EPI_SWIGLU: if constexpr (pairable) return launch_pp<TL, EPI_SWIGLU>(a, st); else return hipErrorInvalidValue;
-    case EPI_GLU: if constexpr (pairable) return launch_pp<TL, EPI_GLU>(a, st); else return hipErrorInvalidValue;
+    case EPI_STORE: return launch_pp<TL, EPI_STORE, RG>(a, st);
+    case EPI_RESID: return launch_pp<TL, EPI_RESID, RG>(a, st);
+    case EPI_SWIGLU: if constexpr (pairable) return launch_pp<TL, EPI_SWIGLU, RG>(a, st); else return hipErrorInvalidValue;
+    case EPI_GLU: if constexpr (pairable) return launch_pp<TL, EPI_GLU, RG>(a, st); else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
@@ -279,6 +317,10 @@ hipError_t gemm_pp(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     case 2: return launch_pp_epi<PT<128, 128, 2, 4, 2, 3>>(a, epi, st);   // 120 KiB
     case 4: return launch_pp_epi<PT<128, 128, 4, 2, 2, 3>>(a, epi, st);   // 120 KiB, 32-row W wave tiles
     case 5: return launch_pp_epi<PT<128, 64, 4, 2, 2, 3>>(a, epi, st);    // 96 KiB
+    // register-staged (global -> VGPR -> ds_write) instead of LDS-DMA
+    case 6: return launch_pp_epi<PT<256, 128, 4, 2, 1, 4>, true>(a, epi, st);
+    case 7: return launch_pp_epi<PT<256, 128, 4, 2, 1, 3>, true>(a, epi, st);
+    case 8: return launch_pp_epi<PT<128, 128, 2, 4, 2, 3>, true>(a, epi, st);
     default: return hipErrorInvalidValue;
   }
 }
