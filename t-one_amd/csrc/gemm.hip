@@ -941,15 +941,23 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   // (gemm_t.hip gemm_p_kernel; FFN up M = 20480: 72.9 vs 82.1 us, pw1 20.1 vs 22.5 us for gemm_t,
   // scripts/gp_sweep.sh, profiles/r02_gemm_p_sweep.jsonl)
   // TONE_GEMM_P (experiments): bit 0 SwiGLU, bit 1 GLU on gemm_p; low nibble of bits 4.. = gemm_p variant
+  // Default now off: the in-step A/B of this tree (scripts/ab_env.py, profiles/r02_ab_ffnup.jsonl) has the 2-stage
+  // transposed kernel ahead at every batch (B = 2048: 6.38 vs 6.74 ms/step; B = 512: 2.57 vs 2.86)
   const char* route_env = getenv("TONE_GEMM_P");
-  const int route = route_env ? atoi(route_env) : 1;   // in-step A/B (scripts/ab_route.py): SwiGLU only, plain stores
+  const int route = route_env ? atoi(route_env) : 0;
   // default variant 7: 2D XCD blocks with 4 n-groups where the tiles divide evenly (87.6-90.9 vs 88-93 us at
   // M = 20480, 166 vs 182 at 40960; profiles/r02_gemm_p_xcd.txt), else the XCD-contiguous order
   const int pv0 = (route >> 4) & 15;
   const int pv = (pv0 == 0 && (a.N / 256) % 4 == 0 && ((a.M + 255) / 256) % 2 == 0) ? 7 : pv0;
+  // TONE_SWIGLU_T = 1 + gemm_t variant (experiments): FFN up on the transposed 2-stage kernel at every M
+  const char* swt = getenv("TONE_SWIGLU_T");
+  if (epi == EPI_SWIGLU && swt && atoi(swt) > 0 && a.N % 256 == 0) return gemm_t(a, epi, atoi(swt) - 1, st);
   if (epi == EPI_SWIGLU && (route & 1) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
   if (epi == EPI_GLU && (route & 2) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
-  if (epi == EPI_SWIGLU && a.N % 256 == 0 && t256 >= 192) return gemm_t(a, epi, 0, st);
+  // FFN up: 256 x 256 tiles once there are ~180 of them (M >= 3840 at N = 3072), 256 W x 128 X rows below that
+  // down to ~200 tiles (M = 2560: 14.5 vs 20.2 us; tools/gemm_bench, profiles/r02_ffnup_route.jsonl)
+  if (epi == EPI_SWIGLU && a.N % 256 == 0 && t256 >= 180) return gemm_t(a, epi, 0, st);
+  if (epi == EPI_SWIGLU && a.N % 256 == 0 && (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200) return gemm_t(a, epi, 2, st);
   if (epi == EPI_GLU && a.N % 128 == 0 && (int64_t)((a.M + 127) / 128) * (a.N / 128) >= 512) return gemm_t(a, epi, 5, st);
   const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);
   const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
