@@ -963,6 +963,10 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
   // 8 waves of 32x64 per 128x128 tile once there is a tile per CU (tools/gemm_bench sweep)
   if (t128 >= kTarget / 2) return launch_glds_epi<Tile<128, 128, 4, 2>>(a, epi, 1, st);
+  // pw1 (GLU, N = 768) at config 4's per-GPU batch of 512 (M = 5120: 10.3 vs 11.1 us; M = 2560 on 64x128 tiles:
+  // 8.5 vs 9.7; profiles/r02_b512_sweep.jsonl)
+  if (epi == EPI_GLU && t128 >= 200) return launch_glds_epi<Tile<128, 128, 4, 2>>(a, epi, 1, st);
+  if (epi == EPI_GLU && t64 >= 200) return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, 1, st);
   // half-chip M (the reduced layers at B = 2048): 64x128 LDS-DMA tiles (scripts/bf16_resid_sweep.sh)
   if ((epi == EPI_STORE || epi == EPI_RESID) && t64 >= kTarget / 2) return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, 1, st);
   if ((epi == EPI_STORE || epi == EPI_RESID) && t64 < kTarget && a.N % 64 == 0 && a.ldc % 8 == 0 && a.lda % 8 == 0 &&

@@ -121,21 +121,25 @@ __device__ __forceinline__ int mx_swz(int r) { return (r >> 1) & 7; }
 
 // DBG (microbenchmark ablations only): bit 0 no epilogue, bit 1 side data (scales, bias, row factors)
 // loaded for the first tile only, bit 2 no MFMA; every accumulator stays live
-template <int BNW, int EPI, bool RS, int DBG = 0>
+// BMX: X rows per tile (256, or 128 for STORE / RESID when the 256-row tiles would leave the CUs one tile each:
+// two tiles per CU overlap one tile's HBM-bound epilogue with the next one's K loop); waves WNW (W) x WMW (X)
+template <int BNW, int EPI, bool RS, int DBG = 0, int BMX = 256>
 __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
-  constexpr int BK = 128, QB = 128 * BK, NQW = BNW / 128, STG = (NQW + 2) * QB;
-  constexpr int TI = BNW / 32, TH = TI / 2;                  // n-tiles per wave, per phase half
+  constexpr int BK = 128, QB = 128 * BK, NQW = BNW / 128, XQ = BMX / 128, STG = (NQW + XQ) * QB;
+  constexpr int WMW = BMX / 64, WNW = 8 / WMW, RW = BNW / WNW;   // waves along X / W, W rows per wave
+  constexpr int TI = RW / 16, TH = TI / 2;                   // n-tiles per wave, per phase half
+  static_assert(TH >= 1 && (EPI != EPI_SWIGLU || TI % 4 == 0), "wave tile");
   constexpr bool PAIRED = (EPI == EPI_SWIGLU);
   static_assert(EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU, "STORE/RESID/SWIGLU");
-  // ONE LDS object: ring | W scales [BNW][48] | X scales [256][48] | bias [BNW] | row factors [256]
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG + (BNW + 256) * kMxKB + 4 * (BNW + 256)];
+  // ONE LDS object: ring | W scales [BNW][48] | X scales [BMX][48] | bias [BNW] | row factors [BMX]
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STG + (BNW + BMX) * kMxKB + 4 * (BNW + BMX)];
   uint8_t* sW = lds + 2 * STG;
   uint8_t* sX = sW + BNW * kMxKB;
-  float* sb = reinterpret_cast<float*>(sX + 256 * kMxKB);
+  float* sb = reinterpret_cast<float*>(sX + BMX * kMxKB);
   float* sr = sb + BNW;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wid >> 2, wm = wid & 3, l15 = lane & 15, lg = lane >> 4, g = mx_swz(l15);
-  const int ntn = p.N / BNW, ntm = (p.M + 255) >> 8, ntiles = ntn * ntm;
+  const int wn = wid / WMW, wm = wid % WMW, l15 = lane & 15, lg = lane >> 4, g = mx_swz(l15);
+  const int ntn = p.N / BNW, ntm = (p.M + BMX - 1) / BMX, ntiles = ntn * ntm;
   const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
   const int q = (ntiles + 7) >> 3, tbeg = xcd * q, tend = min(ntiles, tbeg + q);
   const int nmine = (tbeg + jb < tend) ? (tend - tbeg - jb + nxb - 1) / nxb : 0;
@@ -144,7 +148,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
 
   auto tile_of = [&](int u, int& m0, int& n0) {
     const int t = tbeg + jb + (u / nk) * nxb;
-    m0 = (t / ntn) << 8;
+    m0 = (t / ntn) * BMX;
     n0 = (t % ntn) * BNW;
   };
   // quarter j of K-tile u: W rows 128 j.. (j < NQW) or X rows 128 (j - NQW)..; pieces of 8 rows x 128 B
@@ -178,18 +182,18 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
       const int r = i / KB, c = i % KB;
       sW[r * kMxKB + c] = p.Ws[(int64_t)(n0 + r) * KB + c];
     }
-    for (int i = tid; i < 256 * KB; i += 512) {
+    for (int i = tid; i < BMX * KB; i += 512) {
       const int r = i / KB, c = i % KB;
       sX[r * kMxKB + c] = p.As[(int64_t)min(m0 + r, p.M - 1) * p.ldas + c];
     }
     for (int i = tid; i < BNW; i += 512) sb[i] = p.bias ? p.bias[n0 + i] : 0.f;
     if constexpr (RS)
-      for (int i = tid; i < 256; i += 512) sr[i] = p.rs_inv[min(m0 + i, p.M - 1)];
+      for (int i = tid; i < BMX; i += 512) sr[i] = p.rs_inv[min(m0 + i, p.M - 1)];
   };
 
-  const uint8_t* wq = lds + (wn * BNW / 2 / 128) * QB + ((wn * BNW / 2) % 128) * BK;   // wave's W rows
+  const uint8_t* wq = lds + (wn * RW / 128) * QB + ((wn * RW) % 128) * BK;   // wave's W rows
   const uint8_t* xq = lds + (NQW + (wm >> 1)) * QB + (wm & 1) * 64 * BK;
-  const int wrow0 = wn * BNW / 2, xrow0 = wm * 64;
+  const int wrow0 = wn * RW, xrow0 = wm * 64;
   auto rd = [&](const uint8_t* qb, int buf, int tile) {
     const uint8_t* r = qb + buf * STG + (16 * tile + l15) * BK;
     const u32x4 a = *reinterpret_cast<const u32x4*>(r + 16 * (lg ^ g));
@@ -281,7 +285,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   zero();
   load_side(0);
   __syncthreads();                                              // side data visible; no DMA in flight yet
-  constexpr int QPT = NQW + 2;                                  // quarters per K-tile
+  constexpr int QPT = NQW + XQ;                                 // quarters per K-tile
   // prologue: K-tile 0 whole, the first half of K-tile 1's quarters
   issue_kt(0, 0, QPT);
   if (G > 1) {
@@ -372,9 +376,9 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   }
 }
 
-template <int BNW, int EPI>
+template <int BNW, int EPI, int BMX = 256>
 hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
-  const int ntiles = (a.N / BNW) * ((a.M + 255) / 256);
+  const int ntiles = (a.N / BNW) * ((a.M + BMX - 1) / BMX);
   int grid = 256;
   const int need = ((ntiles + 7) / 8) * 8;
   if (grid > need) grid = need;
@@ -389,8 +393,8 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
       default: return hipErrorInvalidValue;
     }
   }
-  if (a.rs_inv) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true>), dim3(grid), dim3(512), 0, st, a);
-  else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false>), dim3(grid), dim3(512), 0, st, a);
+  if (a.rs_inv) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
   return hipGetLastError();
 }
 
@@ -402,8 +406,16 @@ hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st) {
   if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || (a.ldc % 8) || a.N % 128) return hipErrorInvalidValue;
   switch (epi) {
     case EPI_SWIGLU: return (!a.C8 || !a.C8s) ? hipErrorInvalidValue : launch_mx<128, EPI_SWIGLU>(a, st);
-    case EPI_STORE: return launch_mx<128, EPI_STORE>(a, st);
-    case EPI_RESID: return launch_mx<128, EPI_RESID>(a, st);
+    // 128 X rows per tile while there are few 256-row tiles (FFN down at M = 10240: 22.0 vs 31.7 us, M = 2560-5120:
+    // 18-19 vs 28-30; at M = 20480 the 256-row tile wins 34.4 vs 40.1; q|k|v only below ~128 tiles;
+    // profiles/r02_mx_x128.jsonl).  MXDBG = 16 / 32 force 256 / 128 (tools/gemm_bench)
+    case EPI_STORE:
+    case EPI_RESID: {
+      const int64_t t256 = (int64_t)(a.N / 128) * ((a.M + 255) / 256);
+      const bool x128 = (a.dbg & 32) || (!(a.dbg & 16) && t256 < (epi == EPI_RESID ? 200 : 128));
+      if (epi == EPI_STORE) return x128 ? launch_mx<128, EPI_STORE, 128>(a, st) : launch_mx<128, EPI_STORE>(a, st);
+      return x128 ? launch_mx<128, EPI_RESID, 128>(a, st) : launch_mx<128, EPI_RESID>(a, st);
+    }
     default: return hipErrorInvalidValue;
   }
 }
