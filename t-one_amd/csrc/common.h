@@ -86,6 +86,16 @@ struct StateRef {
   }
 };
 
+// MXFP8 (OCP MX, e4m3 values, one E8M0 scale per 32): the block exponent from the block's max |v|,
+// E = floor(log2 amax) - 8 (biased by 127, clamped), and the inverse block scale 2^(127 - E)
+__device__ __forceinline__ int mx_exp(float amax) {
+  const int e = (int)((__float_as_uint(amax) >> 23) & 0xff);   // biased exponent of amax (0 for 0/subnormal)
+  return max(0, min(254, e - 8));
+}
+__device__ __forceinline__ float exp2i(int ebiased) {
+  return __uint_as_float((uint32_t)(254 - ebiased) << 23);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -12,7 +12,9 @@ constexpr float kInvSqrtD = 0.05103103630798288f;   // 384^-0.5 (submodules.py:5
 // ---------------------------------------------------------------------------------------------
 // RMSNorm (submodules.py:34-54) in place over rows of 384: one wave per row, 6 elements per lane.
 __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, const float* __restrict__ w, int rows,
-                                                      uint16_t* __restrict__ shadow, int64_t plane) {
+                                                      uint16_t* __restrict__ shadow, int64_t plane,
+                                                      uint8_t* __restrict__ q8, uint8_t* __restrict__ s8,
+                                                      float* __restrict__ inv8) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -26,16 +28,36 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, con
   }
   ss = wave_sum(ss);
   const float den = sqrtf(ss) * kInvSqrtD + kRmsEps;
+  float ssq = 0.f;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const float y = w[lane + 64 * i] * (v[i] / den);
     xr[lane + 64 * i] = y;
     if (shadow) store_shadow(shadow, plane, (int64_t)row * kD + lane + 64 * i, y);
+    if (q8) {
+      // fp8 mode: the MXFP8 form of the bf16 shadow row for the next layer's FFN up-projection, as
+      // quant_mx_kernel (gemm_mx.hip) makes it from the shadow: element lane + 64 i lies in 32-block
+      // 2 i + (lane >> 5), whose max |v| is a reduction over its 32 lanes
+      const float vb = (float)(__bf16)y;
+      ssq = fmaf(vb, vb, ssq);
+      float am = fabsf(vb);
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+      const int e = mx_exp(am);
+      const float a = fminf(fmaxf(vb * exp2i(e), -448.f), 448.f);
+      q8[(int64_t)row * kD + lane + 64 * i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(a, 0.f, 0, false) & 0xff);
+      if ((lane & 31) == 0) s8[(int64_t)row * (kD / 32) + 2 * i + (lane >> 5)] = (uint8_t)e;
+    }
+  }
+  if (q8 && inv8) {
+    ssq = wave_sum(ssq);
+    if (lane == 0) inv8[row] = 1.0f / (sqrtf(ssq) * rsqrtf((float)kD) + kRmsEps);
   }
 }
 
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st) {
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane);
+hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st,
+                          uint8_t* q8, uint8_t* s8, float* inv8) {
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, inv8);
   return hipGetLastError();
 }
 

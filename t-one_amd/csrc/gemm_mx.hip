@@ -36,20 +36,12 @@ __device__ __forceinline__ float fsig(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
 
-// E8M0 exponent of an MX block from its max |v|: E = floor(log2 amax) - 8 (biased by 127, clamped)
-__device__ __forceinline__ int mx_exp(float amax) {
-  const int e = (int)((__float_as_uint(amax) >> 23) & 0xff);   // biased exponent of amax (0 for 0/subnormal)
-  return max(0, min(254, e - 8));
-}
 // v / 2^(E - 127) clamped to e4m3's range, two values packed into the low / high half of `w`
 template <bool HI>
 __device__ __forceinline__ uint32_t cvt_pk(float a, float b, float inv, uint32_t w) {
   a = fminf(fmaxf(a * inv, -448.f), 448.f);
   b = fminf(fmaxf(b * inv, -448.f), 448.f);
   return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, (int)w, HI);
-}
-__device__ __forceinline__ float exp2i(int ebiased) {   // 2^(127 - ebiased): the inverse block scale
-  return __uint_as_float((uint32_t)(254 - ebiased) << 23);
 }
 // 8 floats -> 8 e4m3 bytes with the block's inverse scale
 __device__ __forceinline__ u32x2 quant8(const float (&v)[8], float inv) {

@@ -138,7 +138,10 @@ hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, 
 
 // In-place RMSNorm over rows of 384 (norm_out, out_norm); optional bf16 shadow of the result
 // (3 split planes `plane` elements apart when plane > 0).
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st);
+// q8 / s8 / inv8 (fp8 mode, optional): also the MXFP8 form of the bf16 shadow row and its folded-RMSNorm row factor,
+// exactly what launch_quant_mx would make from the shadow
+hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st,
+                          uint8_t* q8 = nullptr, uint8_t* s8 = nullptr, float* inv8 = nullptr);
 
 // Layers 14/15: xn = RMSNorm(r); kv = [cache(S rows) ; xn]; next cache (left-padded to 30) -> state.
 hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S,

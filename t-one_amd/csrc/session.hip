@@ -482,7 +482,15 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, s->w2x, geo.chunk, s->w2p));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * geo.T, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
-  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st));
+  // fp8 mode: the norms that feed a layer's FFN1 directly also emit its MXFP8 operand (no quant_mx launch)
+  // (TONE_FP8_NORMQ=1 turns it on; 0 / unset keeps the separate quant_mx launches -- pending its GPU A/B)
+  static const bool normq = [] {
+    const char* e = std::getenv("TONE_FP8_NORMQ");
+    return e && std::atoi(e) == 1;
+  }();
+  const bool f8n = f8 && normq;
+  bool q8_fresh = f8n;
+  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st, f8n ? s->a8 : nullptr, s->a8s, s->inv8));
   if (s->debug_stop == 1) return TONE_OK;
   float* x = s->rA;
   uint16_t* xs = shA;           // bf16 shadow of x (bf16 mode)
@@ -496,7 +504,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     // up-projection's epilogue
     auto ffn = [&](int f) -> int {
       if (f8) {
-        LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->inv8, st));
+        if (!(f == 0 && q8_fresh)) LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->inv8, st));
+        q8_fresh = false;
         CALL(mx_call(s, st, "gemm_ffn_up", s->a8, s->a8s, w.mx13[f], nullptr, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU,
                      s->inv8, nullptr, 1.0f, false, nullptr, s->h8, s->h8s));
         return mx_call(s, st, "gemm_ffn_down", s->h8, s->h8s, w.mx2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, nullptr, x,
@@ -577,7 +586,9 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
     // FFN2 + norm_out (conformer_blocks.py:832-836)
     CALL(ffn(1));
-    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st));
+    // the next layer's FFN1 reads this norm's output unless the reduction / upsampling comes in between
+    q8_fresh = f8n && l != 6 && l < 14;
+    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->inv8));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
       LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, geo.T, st));
       CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * geo.Tr, D, 4 * D,

@@ -382,6 +382,44 @@ def test_fp8_staggered_streams(weights, oracle):
         s.close()
 
 
+_FP8_PROBE = """
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[2]]
+import tone_amd.config as C
+from tone_amd.model import ToneSession
+from tone_amd.weights import synthetic_weights
+s = ToneSession(synthetic_weights(0), precision="fp8", max_batch=64)
+rng = np.random.default_rng(5)
+st = torch.zeros((64, C.STATE_SIZE), dtype=torch.float16, device=s.dev)
+out = []
+for c in range(3):
+    pcm = np.clip(np.round(rng.normal(0, 3000, (64, C.AUDIO_CHUNK_SAMPLES))), -32768, 32767).astype(np.int32)
+    lp, st = s.step(torch.from_numpy(pcm).to(s.dev), st)
+    out.append(lp.cpu().numpy())
+np.save(sys.argv[1], np.stack(out))
+"""
+
+
+def test_fp8_norm_quant_fusion_matches_quant_mx(tmp_path):
+    """fp8 mode: the RMSNorm kernels that feed a layer's FFN1 emit its MXFP8 operand themselves; the result must
+    match the separate quant_mx launches (TONE_FP8_NORMQ=0) -- same e4m3 values and scales, the row factor up to
+    its summation order -- over 3 stateful chunks."""
+    _gpu()
+    import os
+    import subprocess
+    import sys
+    root = str(Path(__file__).resolve().parents[1])
+    res = {}
+    for flag in ("1", "0"):
+        f = tmp_path / f"lp{flag}.npy"
+        env = dict(os.environ, TONE_FP8_NORMQ=flag)
+        subprocess.run([sys.executable, "-c", _FP8_PROBE, str(f), root], env=env, check=True, timeout=240)
+        res[flag] = np.load(f)
+    d = float(np.abs(res["1"] - res["0"]).max())
+    assert d < 2e-3, d
+    assert np.mean(res["1"].argmax(-1) == res["0"].argmax(-1)) > 0.999
+
+
 @pytest.mark.parametrize("prec,b", [("fp32", 300), ("bf16", 1000), ("fp8", 1000)])
 def test_ragged_batches(weights, oracle, prec, b):
     """Batch sizes that are not multiples of any GEMM tile and cross the launchers' routing thresholds:
