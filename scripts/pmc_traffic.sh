@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   d=gpurun_out/pmc_${prec}/$(echo $c | tr A-Z a-z | cut -d_ -f1)
   rm -rf $d
-  timeout -s KILL 240 rocprofv3 --pmc $c -d $d -o run --output-format csv -- python bench.py --precision $prec --batch $B --steps 2 --warmup 1 --no-graph --cpu-baseline-s 0 --alt 0 > gpurun_out/pmc_${prec}_$c.log 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc $c -d $d -o run --output-format csv -- python bench.py --precision $prec --batch $B --steps 2 --warmup 1 --no-graph --cpu-baseline-s 0 --alt 0 --config4 0 --config5 0 > gpurun_out/pmc_${prec}_$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 exit 0

@@ -7,7 +7,7 @@ import csv, glob, json, re, sys
 
 root, prec, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
 PAT = {  # SWIGLU instantiations: EPI_SWIGLU = 2
-    "fp32": re.compile(r"gemm_x3_kernel<.*XT<\d+, \d+, \d+, \d+, \d+, \d+>, 2, (true|false), (true|false)>"),
+    "fp32": re.compile(r"gemm_x3_kernel<.*XT<\d+, \d+, \d+, \d+, \d+, \d+>, 2, (true|false), (true|false)(, (true|false))*>"),
     "fp32-mfma": re.compile(r"gemm_kernel<tone::Tile<\d+, \d+, \d+, \d+>, 2,"),
     "bf16": re.compile(r"gemm_t_kernel<.*TT<\d+, \d+, \d+, \d+>, 2, (true|false)>"),
 }[prec]

@@ -483,15 +483,20 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * geo.T, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
   // fp8 mode: the norms that feed a layer's FFN1 directly also emit its MXFP8 operand (no quant_mx launch)
-  // (TONE_FP8_NORMQ=1 turns it on; 0 / unset keeps the separate quant_mx launches -- pending its GPU A/B)
+  // (TONE_FP8_NORMQ=0 keeps the separate quant_mx launches; the operands are bit-identical either way,
+  // tests/test_gpu_parity.py::test_fp8_norm_quant_fusion_matches_quant_mx; 0.6-1 % per step, profiles/r02_fp8_normq_ab.txt)
   static const bool normq = [] {
     const char* e = std::getenv("TONE_FP8_NORMQ");
-    return e && std::atoi(e) == 1;
+    return !(e && std::atoi(e) == 0);
   }();
   const bool f8n = f8 && normq;
   bool q8_fresh = f8n;
   LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st, f8n ? s->a8 : nullptr, s->a8s, s->inv8));
-  if (s->debug_stop == 1) return TONE_OK;
+  if (s->debug_stop == 1) {
+    // the fused-vs-separate check reads the first FFN1's MXFP8 operand here: make it the separate way too
+    if (f8 && !f8n) LAUNCH("quant_mx", launch_quant_mx(shA, D, B * geo.T, D, s->a8, s->a8s, s->inv8, st));
+    return TONE_OK;
+  }
   float* x = s->rA;
   uint16_t* xs = shA;           // bf16 shadow of x (bf16 mode)
   int T = geo.T;
@@ -1072,15 +1077,19 @@ int tone_session_debug_read(tone_session* s, const char* buffer, void* host_dst,
   if (!s->finalized) return fail(TONE_E_STATE, "session not finalized");
   const size_t MB = (size_t)s->max_batch;
   const std::string n(buffer);
-  const float* p = nullptr;
-  size_t cap = 0;
-  if (n == "feats") { p = s->feats; cap = MB * kMelTMax * kMels; }
-  else if (n == "x2") { p = static_cast<const float*>(s->x2); cap = MB * kSub2InMax * kSub1F * kSub1C; }
-  else if (n == "flat") { p = static_cast<const float*>(s->flat); cap = MB * kTMax * kSubOut; }
-  else if (n == "rA") { p = s->rA; cap = MB * kTMax * kD; }
-  else if (n == "rB") { p = s->rB; cap = MB * kTrMax * kD; }
+  const void* p = nullptr;
+  size_t cap = 0;   // bytes
+  if (n == "feats") { p = s->feats; cap = MB * kMelTMax * kMels * 4; }
+  else if (n == "x2") { p = s->x2; cap = MB * kSub2InMax * kSub1F * kSub1C * 4; }
+  else if (n == "flat") { p = s->flat; cap = MB * kTMax * kSubOut * 4; }
+  else if (n == "rA") { p = s->rA; cap = MB * kTMax * kD * 4; }
+  else if (n == "rB") { p = s->rB; cap = MB * kTrMax * kD * 4; }
+  // fp8 mode: the MXFP8 operand of the next MX GEMM (e4m3 [M][384], E8M0 [M][12], fp32 row factors [M])
+  else if (n == "a8" && s->a8) { p = s->a8; cap = MB * kTMax * kD; }
+  else if (n == "a8s" && s->a8s) { p = s->a8s; cap = MB * kTMax * (kD / 32); }
+  else if (n == "inv8" && s->inv8) { p = s->inv8; cap = MB * kTMax * 4; }
   else return fail(TONE_E_INVALID, "unknown debug buffer " + n);
-  if ((size_t)bytes > cap * sizeof(float)) return fail(TONE_E_INVALID, "debug_read larger than the buffer");
+  if ((size_t)bytes > cap) return fail(TONE_E_INVALID, "debug_read larger than the buffer");
   HIP_TRY(hipSetDevice(s->device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(host_dst, p, (size_t)bytes, hipMemcpyDeviceToHost));

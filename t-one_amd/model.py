@@ -206,8 +206,8 @@ class ToneSession:
     def debug_stop(self, stage: int) -> None:
         _lib.check(self._lib.tone_session_debug_stop(self._h, int(stage)), "tone_session_debug_stop")
 
-    def debug_read(self, name: str, shape) -> np.ndarray:
-        out = np.empty(shape, np.float32)
+    def debug_read(self, name: str, shape, dtype=np.float32) -> np.ndarray:
+        out = np.empty(shape, dtype)
         _lib.check(self._lib.tone_session_debug_read(self._h, name.encode(), out.ctypes.data_as(ctypes.c_void_p),
                                                      out.nbytes), f"tone_session_debug_read({name})")
         return out
