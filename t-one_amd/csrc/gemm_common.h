@@ -50,7 +50,7 @@ __device__ __forceinline__ void barrier_lds() {   // keeps LDS-DMA in flight (no
 // bf16: pack to 4-element runs, swap runs between the lane halves (T21) so each lane owns 8
 // contiguous elements, and store 2 x 16 B.  rowp points at column c of row m.  All lanes must
 // execute the swaps; only the store is predicated.
-__device__ __forceinline__ void store_tile_bf16(uint16_t* rowp, const float (&v)[16], int lh, bool ok) {
+__device__ __forceinline__ void store_tile_bf16(uint16_t* rowp, const float (&v)[16], int lh, bool ok, bool nt = false) {
   uint32_t px[4], py[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -62,7 +62,11 @@ __device__ __forceinline__ void store_tile_bf16(uint16_t* rowp, const float (&v)
     const auto rx = __builtin_amdgcn_permlane32_swap(px[k], px[k + 1], false, false);
     const auto ry = __builtin_amdgcn_permlane32_swap(py[k], py[k + 1], false, false);
     const u32x4 o = {rx[0], ry[0], rx[1], ry[1]};
-    if (ok) *reinterpret_cast<u32x4*>(rowp + 8 * k + 8 * lh) = o;
+    if (ok) {
+      // nt: streaming output (the FFN intermediate h) kept from displacing the operands in L2
+      if (nt) __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(rowp + 8 * k + 8 * lh));
+      else *reinterpret_cast<u32x4*>(rowp + 8 * k + 8 * lh) = o;
+    }
   }
 }
 
@@ -104,7 +108,7 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
           else o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);   // fp32 output: IEEE exp/div
         }
         if (p.c_bf16) {
-          store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, o, lh, ok);
+          store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, o, lh, ok, p.nt_store != 0);
         } else if (p.c_plane) {   // fp32 split mode: the next GEMM's A as 3 bf16 planes
           store_tile_split(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, p.c_plane, o, lh, ok);
         } else {
