@@ -955,6 +955,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
     }
   };
 
+  // dbg 64 (set by launch_x3): static priority for the second-dispatched half of the waves, the arbitration
+  // loser of every segment (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if ((p.dbg & 64) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   if constexpr (S == 3) {
     stage(0, 0);
     if (nk > 1) stage(1, 1);
@@ -1043,6 +1046,12 @@ template <class TL, int EPI>
 hipError_t launch_x3(const GemmArgs& a0, hipStream_t st) {
   GemmArgs a = a0;
   a.xcd_a = x3_xcd_split<TL>(a0);
+  {
+    // static priority for waves NW/2.. (default; TONE_X3_PRIO=0 turns it off, read per launch for in-process A/B):
+    // fp32 B = 256 step 3.616 -> 3.583 ms, FFN down 897 -> 871 us (scripts/ab_env.py, profiles/r02_ab_x3_prio.jsonl)
+    const char* e = std::getenv("TONE_X3_PRIO");
+    if (!(e && std::atoi(e) == 0)) a.dbg |= 64;
+  }
   const dim3 tiles((a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX), a.k_split ? a.K / a.k_split : 1);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
   // TONE_X3_HL=1: half the waves issue the LDS-DMA (A/B only: 10-40 % slower on every B = 256 shape --
