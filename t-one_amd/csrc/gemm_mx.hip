@@ -19,6 +19,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace tone {
 namespace {
 
@@ -130,6 +132,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   float* sb = reinterpret_cast<float*>(sX + BMX * kMxKB);
   float* sr = sb + BNW;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (p.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);   // static priority, second half (gemm_mx() sets prio)
   const int wn = wid / WMW, wm = wid % WMW, l15 = lane & 15, lg = lane >> 4, g = mx_swz(l15);
   const int ntn = p.N / BNW, ntm = (p.M + BMX - 1) / BMX, ntiles = ntn * ntm;
   const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
@@ -392,7 +395,12 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
 
 }  // namespace
 
-hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st) {
+hipError_t gemm_mx(const MxArgs& a0, int epi, hipStream_t st) {
+  MxArgs a = a0;
+  {
+    const char* e = std::getenv("TONE_PRIO_MX");   // read per call: in-process A/B (scripts/ab_env.py)
+    a.prio = e && std::atoi(e) == 1;
+  }
   // 128 W rows per tile: the 256-row tile needs 96 fragment VGPRs per wave at 32 bytes per lane and
   // spills at two waves per SIMD
   if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || (a.ldc % 8) || a.N % 128) return hipErrorInvalidValue;

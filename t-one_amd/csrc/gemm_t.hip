@@ -48,6 +48,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_t_kernel(GemmArgs p
   float* sbias = rden + 2 * BMX;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (p.prio && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);   // static priority, second half (gemm() sets prio)
   const int wn = wid / WM, wm = wid % WM;
   const int lr = lane & 31, lh = lane >> 5, cs = (lr >> 1) & 7;
   const int ntn = p.N / BNW, ntm = (p.M + BMX - 1) / BMX, ntiles = ntn * ntm;

@@ -45,6 +45,7 @@ struct GemmArgs {
   int64_t c_plane;    // STORE / SWIGLU / GLU: C written as 3 bf16 planes instead of fp32
   int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
   int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
+  int prio;           // bf16 kernels: static priority for the second half of the waves (set by gemm(), TONE_PRIO_BF16)
   const uint16_t* W3b; // fp32 mode: the same planes K16-blocked, [3][K/16][N][16] (gemm_pp), or nullptr
   int xcd_a;          // gemm_x3: XCD x owns the 2D tile block (n-group x % a, m-group x / a) of an a x (8 / a)
                       // split (set by the launcher; 0 = the default order)
@@ -75,6 +76,7 @@ struct MxArgs {
   int64_t ldc8s;
   int M, N, K;
   int dbg;                // microbenchmarks only (gemm_mx.hip DBG bits); 0 in the session
+  int prio;               // static priority for waves 4-7 (set by gemm_mx(), TONE_PRIO_MX)
 };
 hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st);
 // bf16 [M][K] (ldx elements) -> e4m3 [M][K] + E8M0 [M][K/32]; inv (optional): 1/(||row||/sqrt(K) + 1e-8)
