@@ -1,12 +1,16 @@
 """Import shim: exposes the package directory ``t-one_amd/`` as the importable name ``tone_amd``.
 
-``t-one_amd`` is not a valid Python identifier, so this module turns itself into that package
-(a module with ``__path__`` is a package) and runs the package ``__init__``.
+``t-one_amd`` is not a valid Python identifier.  Importing this module loads that directory as a
+regular package through importlib (a spec with ``submodule_search_locations``, so ``tone_amd.model``
+etc. resolve inside it) and puts the package in ``sys.modules`` under this name, which is what the
+``import`` statement then returns.
 """
+import importlib.util as _ilu
 import os as _os
+import sys as _sys
 
-__package__ = __name__
-__path__ = [_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "t-one_amd")]
-_init = _os.path.join(__path__[0], "__init__.py")
-with open(_init, encoding="utf-8") as _f:
-    exec(compile(_f.read(), _init, "exec"))
+_dir = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "t-one_amd")
+_spec = _ilu.spec_from_file_location(__name__, _os.path.join(_dir, "__init__.py"), submodule_search_locations=[_dir])
+_pkg = _ilu.module_from_spec(_spec)
+_sys.modules[__name__] = _pkg
+_spec.loader.exec_module(_pkg)
