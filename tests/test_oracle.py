@@ -214,3 +214,98 @@ def test_oracle_400ms_stream_matches_forward_for_export():
         ref = g["logprobs"][:, c]
         assert np.abs(lp - ref).max() < 3e-4, (c, np.abs(lp - ref).max())
         np.testing.assert_array_equal(lp.argmax(-1), ref.argmax(-1))
+
+
+# ---- the exported graph's fp16 numerics (tests/golden/make_golden_fp16.py, oracle/tone_oracle_fp16.py) ----
+def _h(x):
+    return np.asarray(x, np.float32).astype(np.float16).astype(np.float32)
+
+
+def test_fp16_rounding_semantics_match_torch_cpu():
+    """The rounding points tone_oracle_fp16 restates, checked bit for bit against torch's own CPU fp16 kernels
+    (the ones the export traced): fp16 addmm = fp32-accumulated product + fp16 bias rounded once; true
+    division by a Python scalar; softmax with an fp32 sum; log_softmax with the exp-sum AND its log kept in
+    fp16.  SiLU / GLU / BatchNorm are the fp32 formula rounded once (a handful of last-bit exp differences)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(0)
+    x = torch.from_numpy(rng.normal(0, 3, (64, 384)).astype(np.float16))
+    xf = x.float().numpy()
+    w = torch.from_numpy(rng.normal(0, 0.05, (256, 384)).astype(np.float16))
+    b = torch.from_numpy(rng.normal(0, 0.1, 256).astype(np.float16))
+    np.testing.assert_array_equal(torch.addmm(b, x, w.T).float().numpy(),
+                                  _h(xf @ w.float().numpy().T + b.float().numpy()))
+    np.testing.assert_array_equal((x / np.sqrt(48.0)).float().numpy(), _h(xf / np.float32(np.sqrt(48.0))))
+    m = xf.max(-1, keepdims=True)
+    e = np.exp(xf - m)
+    np.testing.assert_array_equal(torch.softmax(x, -1).float().numpy(), _h(e / e.sum(-1, keepdims=True)))
+    lse = _h(np.log(_h(e.sum(-1, keepdims=True))))
+    np.testing.assert_array_equal(torch.log_softmax(x, -1).float().numpy(), _h(xf - m - lse))
+    silu = torch.nn.functional.silu(x).float().numpy()
+    assert np.mean(silu != _h(xf / (np.float32(1) + np.exp(-xf)))) < 1e-3
+
+
+@pytest.fixture(scope="module")
+def fp16_runs():
+    """The golden streams through the fp16 oracle with fp32 (numpy sgemm, torch's order) and fp64 accumulation."""
+    from tone_oracle_fp16 import ToneOracleFP16
+    g = np.load(GOLDEN / "golden_stream.npz")
+    pcm = g["pcm"].astype(np.int32)
+    B, N = pcm.shape[:2]
+    W = synthetic_weights(0)
+    out = {}
+    for acc in ("f32", "f64"):
+        orc = ToneOracleFP16(W, acc)
+        st = np.zeros((B, C.STATE_SIZE), np.float16)
+        lps = []
+        for c in range(N):
+            st[np.arange(B) > c] = 0
+            lp, st = orc.step(pcm[:, c], st)
+            lps.append(lp)
+        out[acc] = np.stack(lps, 1)
+    return out
+
+
+def test_fp16_oracle_matches_exported_graph(fp16_runs):
+    """tone_oracle_fp16 against Tone.forward_for_export with the export's numerics (golden_fp16.npz): every
+    logprob within two fp16 ulps of the graph's (|lp| < 16: 2 x 7.8e-3), mean 3.1e-3 measured, ~42 % of the
+    logprobs bit-identical, argmax identical everywhere.  The oracle has the graph's rounding points; what it
+    cannot have is the exporting machine's summation order inside each conv / GEMM (numpy's sgemm equals torch's
+    addmm, its im2col convolutions do not equal oneDNN's), and an fp32 last-bit difference in front of an fp16
+    rounding point lands on the neighbouring fp16 value -- see the floor test below."""
+    ref = np.load(GOLDEN / "golden_fp16.npz")["stream_logprobs"]
+    d = np.abs(fp16_runs["f32"] - ref)
+    assert d.max() <= 2 * 7.8125e-3 and d.mean() < 5e-3, (d.max(), d.mean())
+    assert np.mean(d == 0) > 0.3
+    np.testing.assert_array_equal(fp16_runs["f32"].argmax(-1), ref.argmax(-1))
+
+
+def test_fp16_summation_order_floor(fp16_runs):
+    """The measured floor of "<= 1e-3 against the fp16 graph": two implementations with IDENTICAL rounding
+    points that differ only in the summation order inside the contractions (fp32 vs fp64 accumulation) already
+    disagree by 1.56e-2 max, 3.1e-3 mean (p99 1.2e-2) on these streams -- as far apart as either is from the
+    torch trace.  The first divergence is the first rounding point: 0.09 % of the fp16 features (7 of 7680
+    values in one step) round the other way, and every later fp16 rounding multiplies the flips (30 % of the
+    pre-encode output differs by one ulp).  So no implementation short of a bitwise clone of the exporting
+    machine's kernels -- ORT's MLAS kernels included -- can hold 1e-3 against the fp16 graph; the 1e-3 bar
+    is held against the fp32 semantics (test_stream_matches_reference_step, GPU test_golden_stream_parity)."""
+    d = np.abs(fp16_runs["f32"] - fp16_runs["f64"])
+    assert 5e-3 < d.max() <= 2 * 7.8125e-3 and d.mean() > 1e-3, (d.max(), d.mean())
+    np.testing.assert_array_equal(fp16_runs["f32"].argmax(-1), fp16_runs["f64"].argmax(-1))
+
+
+def test_fp16_oracle_stages_track_the_graph():
+    """One step from a carried state, stage by stage against the graph's own fp16 values (forward hooks):
+    features >= 99.8 % bit-identical; the encoder stages drift by flips alone -- relative L2 error growing
+    from 2.8e-4 (pre-encode) to 1.3e-3 (layer 13), max 8.8e-3 on values up to 5.8 (a few fp16 ulps), about
+    one fp16 half-ulp of relative error per layer."""
+    from tone_oracle_fp16 import ToneOracleFP16
+    g = np.load(GOLDEN / "golden_fp16.npz")
+    trace = []
+    ToneOracleFP16(synthetic_weights(0)).step(g["step_pcm"].astype(np.int32), g["step_state_in"], trace=trace)
+    feats = g["step_feats"].astype(np.float32).transpose(0, 2, 1)
+    assert np.mean(trace[0] == feats) > 0.998
+    ref = g["step_stages"].astype(np.float32)
+    for i, t in enumerate(trace[1:]):
+        r = ref[:, i, : t.shape[1]]
+        rel = np.linalg.norm(t - r) / np.linalg.norm(r)
+        assert rel < 2.5e-3 and np.abs(t - r).max() < 1.6e-2, f"stage {i}: rel {rel:.3g}"
