@@ -281,15 +281,21 @@ class StreamingCTCModel:
 
     @classmethod
     def from_hugging_face(cls, **kw) -> "StreamingCTCModel":
-        """tone/onnx_wrapper.py:38-50 -- resolves ``model.onnx`` through the HF cache."""
+        """tone/onnx_wrapper.py:38-50: the t-tech/T-one weights through the HF cache (see
+        :meth:`download_from_hugging_face` for which file)."""
         return cls.from_local(cls.download_from_hugging_face(), **kw)
 
     @classmethod
     def download_from_hugging_face(cls) -> str:
-        """tone/onnx_wrapper.py:52-63: ``hf_hub_download("t-tech/T-one", "model.onnx")`` (works offline
-        when the file is already in the HF cache)."""
+        """tone/onnx_wrapper.py:52-63 fetches ``model.onnx``.  The torch checkpoint of the same model,
+        ``model.safetensors``, carries every parameter under its own name, so it is tried first; ``model.onnx``
+        (read by :mod:`tone_amd.onnx_weights`, which attributes constant-folded initializers through the graph)
+        is the fallback.  Offline this works when either file is already in the HF cache."""
         from huggingface_hub import hf_hub_download
-        return hf_hub_download(cls.HF_REPO, cls.HF_MODEL)
+        try:
+            return hf_hub_download(cls.HF_REPO, cls.HF_WEIGHTS)
+        except Exception:      # not published / not cached offline: the reference's own artifact
+            return hf_hub_download(cls.HF_REPO, cls.HF_MODEL)
 
     @classmethod
     def from_local(cls, model_path: str | Path, providers: Optional[list[str]] = None, *, device: int = 0,

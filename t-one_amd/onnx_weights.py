@@ -14,11 +14,25 @@ Fields used (onnx.proto, IR version >= 3):
 * ``TensorProto``: 1 dims, 2 data_type, 4 float_data, 5 int32_data, 7 int64_data, 8 name,
   9 raw_data, 10 double_data, 14 data_location (1 = EXTERNAL, not supported)
 
-Mapping onto the reference ``state_dict`` names (:data:`tone_amd.weights.PARAM_SHAPES`): an
-initializer named like a parameter (optionally prefixed ``tone.``, as the HF ``ToneForCTC`` export
-does) is taken as is, or transposed when it holds the ``[in, out]`` MatMul form of a Linear weight.
-Constant-folded initializers with generated names (``onnx::MatMul_123``) cannot be attributed to a
-parameter from the file alone; :func:`load_onnx_weights` then names the missing parameters in its error.
+Mapping onto the reference ``state_dict`` names (:data:`tone_amd.weights.PARAM_SHAPES`) follows the GRAPH,
+because ``torch.onnx.export`` as tone/scripts/export.py:469-498 calls it (constant folding on, under fp16
+autocast, the model wrapped as ``ModelToExport._model``, export.py:144) does not keep parameter names:
+
+* an initializer still named like a parameter (prefix ``_model.`` / ``tone.`` stripped) is taken by name;
+* any other float initializer (``onnx::MatMul_123``, a folded ``Cast`` output, ...) is attributed through
+  the node that consumes it -- following ``Cast`` / ``Identity`` / ``Transpose`` / ``Reshape`` /
+  ``Unsqueeze`` / ``Squeeze`` chains -- whose name carries the module scope
+  (``/_model/encoder/layers.0/feed_forward1/linear1/MatMul`` -> ``encoder.layers.0.feed_forward1.linear1``)
+  and whose operator fixes the role and the ORIENTATION: ``MatMul`` input B holds ``[in, out]`` (transposed
+  back -- square q/k/v/out weights included, which a shape test cannot tell), ``Gemm`` follows ``transB``,
+  a ``Transpose`` on the way applies its ``perm``; ``Conv`` inputs 1 / 2 are weight / bias; ``Add`` after
+  a MatMul is the bias; ``BatchNormalization`` inputs 1-4 and ``LayerNormalization`` inputs 1-2 are the norm
+  parameters; ``Mul`` is an RMSNorm gain;
+* a BatchNorm the exporter fused into its convolution (eval-mode Conv+BatchNormalization peephole) leaves
+  no parameters of its own: it is loaded as the identity (gain 1, shift 0, mean 0, var 1 - eps) and the conv
+  carries the fused weight and bias.
+
+Whatever is still unattributed is named in :func:`load_onnx_weights`'s error.
 """
 
 from __future__ import annotations
@@ -156,8 +170,24 @@ def parse_tensor(buf: memoryview) -> tuple[str, np.ndarray]:
     return name, arr.reshape(shape)
 
 
-def read_onnx_tensors(path: str | Path) -> dict[str, np.ndarray]:
-    """All graph initializers plus tensor-valued Constant node outputs of an ONNX model file."""
+def _attr_value(buf) -> tuple[str, object]:
+    """AttributeProto -> (name, int | list[int] | tensor bytes): 1 name, 3 i, 5 t, 8 ints."""
+    name, val, ints = "", None, []
+    for f, wt, v in _fields(buf):
+        if f == 1:
+            name = bytes(v).decode()
+        elif f == 3:
+            val = _signed64(int(v))
+        elif f == 5 and wt == 2:
+            val = v
+        elif f == 8:
+            ints += [_signed64(x) for x in _packed_varints(v, wt)]
+    return name, (ints if ints else val)
+
+
+def read_onnx_graph(path: str | Path) -> tuple[dict[str, np.ndarray], list[dict]]:
+    """Initializers plus tensor-valued Constant node outputs, and every node as
+    ``{"name", "op", "inputs", "outputs", "attrs"}`` (NodeProto: 1 input, 2 output, 3 name, 4 op_type, 5 attribute)."""
     data = memoryview(Path(path).read_bytes())
     graph = None
     for f, wt, v in _fields(data):
@@ -166,52 +196,156 @@ def read_onnx_tensors(path: str | Path) -> dict[str, np.ndarray]:
     if graph is None:
         raise OnnxFormatError(f"{path}: no ModelProto.graph (not an ONNX model?)")
     out: dict[str, np.ndarray] = {}
+    nodes: list[dict] = []
     for f, wt, v in _fields(graph):
         if f == 5 and wt == 2:
             name, arr = parse_tensor(v)
             out[name] = arr
-        elif f == 1 and wt == 2:     # NodeProto: keep Constant(value=tensor)
-            op, outs, tensor = "", [], None
+        elif f == 1 and wt == 2:
+            node = {"name": "", "op": "", "inputs": [], "outputs": [], "attrs": {}}
             for nf, nwt, nv in _fields(v):
-                if nf == 4:
-                    op = bytes(nv).decode()
+                if nf == 1:
+                    node["inputs"].append(bytes(nv).decode())
                 elif nf == 2:
-                    outs.append(bytes(nv).decode())
+                    node["outputs"].append(bytes(nv).decode())
+                elif nf == 3:
+                    node["name"] = bytes(nv).decode()
+                elif nf == 4:
+                    node["op"] = bytes(nv).decode()
                 elif nf == 5:
-                    aname, at = "", None
-                    for af, awt, av in _fields(nv):
-                        if af == 1:
-                            aname = bytes(av).decode()
-                        elif af == 5 and awt == 2:
-                            at = av
-                    if aname == "value" and at is not None:
-                        tensor = at
-            if op == "Constant" and tensor is not None and outs:
-                _, arr = parse_tensor(tensor)
-                out.setdefault(outs[0], arr)
-    return out
+                    an, av = _attr_value(nv)
+                    node["attrs"][an] = av
+            if node["op"] == "Constant" and isinstance(node["attrs"].get("value"), memoryview) and node["outputs"]:
+                _, arr = parse_tensor(node["attrs"]["value"])
+                out.setdefault(node["outputs"][0], arr)
+            nodes.append(node)
+    return out, nodes
 
 
-def onnx_state_dict(tensors: dict[str, np.ndarray]) -> dict[str, np.ndarray]:
-    """Map ONNX tensors onto reference parameter names (PARAM_SHAPES), float32.
+def read_onnx_tensors(path: str | Path) -> dict[str, np.ndarray]:
+    """All graph initializers plus tensor-valued Constant node outputs of an ONNX model file."""
+    return read_onnx_graph(path)[0]
 
-    Only names that match a parameter (with or without the HF ``tone.`` prefix) are used; a 2-D
-    tensor whose shape is the transpose of the parameter's is the MatMul form of a Linear weight
-    and is transposed back.  Missing parameters are left out (``normalize_keys`` reports them)."""
+
+_PREFIXES = ("_model.", "tone.")                 # ModelToExport._model (export.py:144); HF ToneForCTC.tone
+_PASS = {"Cast", "Identity", "Transpose", "Reshape", "Unsqueeze", "Squeeze", "Flatten"}
+
+
+def _strip(name: str) -> str:
+    for p in _PREFIXES:
+        if name.startswith(p):
+            return name[len(p):]
+    return name
+
+
+def scope_of(node_name: str) -> str:
+    """Module path of a node: ``/_model/encoder/layers.0/conv/pointwise_conv1/Conv`` ->
+    ``encoder.layers.0.conv.pointwise_conv1``.  A segment that repeats its parent as a prefix (the exporter's
+    ``conv.0`` / ``conv.0.0`` form of nested containers) replaces the parent."""
+    segs = [x for x in node_name.split("/") if x][:-1]
+    path: list[str] = []
+    for sg in segs:
+        if path and sg.startswith(path[-1] + "."):
+            path[-1] = sg
+        else:
+            path.append(sg)
+    return _strip(".".join(path))
+
+
+def _roles(node: dict, slot: int, producer_op: str) -> list[str]:
+    """Parameter role(s) of input ``slot`` of ``node``."""
+    op = node["op"]
+    if op in ("MatMul", "Gemm", "Conv"):
+        return ["weight"] if slot == 1 else (["bias"] if slot == 2 else [])
+    if op == "Add":
+        return ["bias"]
+    if op == "BatchNormalization":
+        return {1: ["weight"], 2: ["bias"], 3: ["running_mean"], 4: ["running_var"]}.get(slot, [])
+    if op == "LayerNormalization":
+        return {1: ["weight"], 2: ["bias"]}.get(slot, [])
+    if op == "Mul":
+        return ["weight"]
+    return []
+
+
+def onnx_state_dict(tensors: dict[str, np.ndarray], nodes: list[dict] | None = None) -> dict[str, np.ndarray]:
+    """Map ONNX tensors onto reference parameter names (PARAM_SHAPES), float32 (see the module docstring).
+    Missing parameters are left out (:func:`load_onnx_weights` reports them)."""
     from .weights import PARAM_SHAPES
 
     out: dict[str, np.ndarray] = {}
-    for name, arr in tensors.items():
-        key = name[len("tone."):] if name.startswith("tone.") else name
-        if key not in PARAM_SHAPES or not np.issubdtype(np.asarray(arr).dtype, np.floating):
-            continue
-        want = PARAM_SHAPES[key]
-        a = np.asarray(arr, dtype=np.float32)
-        if a.shape != want and a.ndim == 2 and a.T.shape == want:
+
+    def put(key: str, a: np.ndarray, transposed: bool) -> bool:
+        want = PARAM_SHAPES.get(key)
+        if want is None or key in out:
+            return False
+        a = np.asarray(a, dtype=np.float32)
+        if transposed and a.ndim == 2:
             a = a.T
-        elif a.shape != want and a.size == int(np.prod(want)) and a.ndim < len(want):
-            a = a.reshape(want)   # e.g. a 1x1 conv stored as its [out, in] matrix
+        if a.shape != want:
+            if a.size != int(np.prod(want)) or a.ndim >= len(want):
+                return False
+            a = a.reshape(want)          # e.g. a 1x1 conv stored as its [out, in] matrix
         out[key] = np.ascontiguousarray(a)
+        return True
+
+    floats = {k: v for k, v in tensors.items() if np.issubdtype(np.asarray(v).dtype, np.floating)}
+    # 1) by name
+    for name, arr in floats.items():
+        key = _strip(name)
+        if key in PARAM_SHAPES:
+            want = PARAM_SHAPES[key]
+            put(key, arr, np.asarray(arr).shape != want and np.asarray(arr).ndim == 2 and np.asarray(arr).T.shape == want)
+    if not nodes:
+        return out
+    # 2) through the consuming node's scope
+    consumers: dict[str, list[tuple[dict, int]]] = {}
+    for nd in nodes:
+        for i, x in enumerate(nd["inputs"]):
+            consumers.setdefault(x, []).append((nd, i))
+    for name, arr in floats.items():
+        if _strip(name) in PARAM_SHAPES:
+            continue
+        # follow pass-through ops to the first compute node; track transposes
+        frontier = [(name, False, 0)]
+        seen = set()
+        while frontier:
+            val, tr, depth = frontier.pop()
+            if val in seen or depth > 6:
+                continue
+            seen.add(val)
+            for nd, slot in consumers.get(val, []):
+                if nd["op"] in _PASS:
+                    t = tr
+                    if nd["op"] == "Transpose":
+                        perm = nd["attrs"].get("perm")
+                        t = tr ^ (perm is None or list(perm)[-2:] == [1, 0] or list(perm) == [1, 0])
+                    for o in nd["outputs"]:
+                        frontier.append((o, t, depth + 1))
+                    continue
+                scope = scope_of(nd["name"])
+                if not scope:
+                    continue
+                transposed = tr
+                if nd["op"] == "MatMul" and slot == 1:
+                    transposed = not tr                                  # B = [in, out]
+                elif nd["op"] == "Gemm" and slot == 1:
+                    transposed = tr ^ (not nd["attrs"].get("transB", 0))
+                for role in _roles(nd, slot, ""):
+                    if put(f"{scope}.{role}", arr, transposed):
+                        frontier = []
+                        break
+    # 3) BatchNorm fused into its convolution by the exporter: identity norm
+    for key in PARAM_SHAPES:
+        if key.endswith(".running_var"):
+            base = key[: -len("running_var")]
+            bn = [base + r for r in ("weight", "bias", "running_mean", "running_var")]
+            if all(k not in out for k in bn):
+                n = PARAM_SHAPES[key][0]
+                out[bn[0]] = np.ones(n, np.float32)
+                out[bn[1]] = np.zeros(n, np.float32)
+                out[bn[2]] = np.zeros(n, np.float32)
+                out[bn[3]] = np.full(n, 1.0 - 1e-5, np.float32)    # 1 / sqrt(var + eps) = 1
     return out
 
 
@@ -219,13 +353,12 @@ def load_onnx_weights(path: str | Path):
     """Parameters of ``model.onnx`` by reference name (raises ValueError naming what is missing)."""
     from .weights import PARAM_SHAPES, normalize_keys
 
-    tensors = read_onnx_tensors(path)
-    sd = onnx_state_dict(tensors)
+    tensors, nodes = read_onnx_graph(path)
+    sd = onnx_state_dict(tensors, nodes)
     missing = [k for k in PARAM_SHAPES if k not in sd]
     if missing:
         raise ValueError(
-            f"{path}: {len(missing)} of {len(PARAM_SHAPES)} T-one parameters are not named initializers of the "
-            f"ONNX graph (e.g. {missing[:3]}); constant-folded exports rename them. Export with "
-            "do_constant_folding=False, or place model.safetensors from t-tech/T-one next to it.")
+            f"{path}: {len(missing)} of {len(PARAM_SHAPES)} T-one parameters could not be attributed to ONNX "
+            f"initializers by name or by their consuming node's scope (e.g. {missing[:3]}). Place model.safetensors "
+            "from t-tech/T-one next to it, or export with do_constant_folding=False.")
     return normalize_keys(sd)
-

@@ -137,7 +137,10 @@ def normalize_keys(sd: dict) -> "OrderedDict[str, np.ndarray]":
     """Map a reference checkpoint (``Tone`` or HF ``ToneForCTC`` keys) onto PARAM_SHAPES names."""
     out: "OrderedDict[str, np.ndarray]" = OrderedDict()
     for k, v in sd.items():
-        kk = k[len("tone."):] if k.startswith("tone.") else k
+        kk = k
+        for pfx in ("_model.", "tone."):   # ModelToExport._model (tone/scripts/export.py:144); HF ToneForCTC.tone
+            if kk.startswith(pfx):
+                kk = kk[len(pfx):]
         if kk.endswith("num_batches_tracked"):
             continue
         if kk not in PARAM_SHAPES:
@@ -149,7 +152,7 @@ def normalize_keys(sd: dict) -> "OrderedDict[str, np.ndarray]":
     missing = [k for k in PARAM_SHAPES if k not in out]
     if missing:
         raise ValueError(f"checkpoint is missing {len(missing)} tensors, e.g. {missing[:3]}")
-    return out
+    return OrderedDict((k, out[k]) for k in PARAM_SHAPES)
 
 
 def load_weights(path: str | Path) -> "OrderedDict[str, np.ndarray]":

@@ -61,6 +61,16 @@ def constant_node(output: str, arr: np.ndarray) -> bytes:
     return _ld(2, output.encode()) + _ld(4, b"Constant") + _ld(5, attr)
 
 
+def node_proto(name: str, op: str, inputs: list[str], outputs: list[str], ints: dict | None = None) -> bytes:
+    """NodeProto: 1 input, 2 output, 3 name, 4 op_type, 5 attribute (AttributeProto 1 name, 3 i, 8 ints)."""
+    msg = b"".join(_ld(1, x.encode()) for x in inputs) + b"".join(_ld(2, x.encode()) for x in outputs)
+    msg += _ld(3, name.encode()) + _ld(4, op.encode())
+    for k, v in (ints or {}).items():
+        a = _ld(1, k.encode()) + (b"".join(_vi(8, x) for x in v) if isinstance(v, list) else _vi(3, v))
+        msg += _ld(5, a)
+    return msg
+
+
 def model_proto(initializers: list[bytes], nodes: list[bytes] = ()) -> bytes:
     graph = b"".join(_ld(1, n) for n in nodes) + _ld(2, b"tone") + b"".join(_ld(5, t) for t in initializers)
     return _vi(1, 8) + _ld(7, graph)
@@ -129,5 +139,134 @@ def test_missing_parameters_are_named(tmp_path):
     inits.append(tensor_proto("onnx::MatMul_1234", np.zeros((384, 1536), np.float16)))
     p = tmp_path / "model.onnx"
     p.write_bytes(model_proto(inits))
-    with pytest.raises(ValueError, match="not named initializers"):
+    with pytest.raises(ValueError, match="could not be attributed"):
         load_weights(p)
+
+
+def _fold_bn(w: dict, conv: str, bn: str):
+    """Eval Conv + BatchNormalization fused the way the exporter's peephole does: W * s, (b - mean) * s + beta."""
+    s = w[bn + "weight"] / np.sqrt(w[bn + "running_var"] + 1e-5)
+    wf = w[conv + "weight"] * s.reshape((-1,) + (1,) * (w[conv + "weight"].ndim - 1))
+    bf = (w[conv + "bias"] - w[bn + "running_mean"]) * s + w[bn + "bias"]
+    return wf.astype(np.float32), bf.astype(np.float32)
+
+
+def export_like_graph(w: dict) -> bytes:
+    """A graph shaped like torch.onnx.export of ModelToExport under fp16 autocast with constant folding
+    (tone/scripts/export.py:144,411,469-498): Linear weights folded into anonymous ``onnx::MatMul_*`` fp16
+    initializers in MatMul's [in, out] form (square q/k/v/out included), biases behind Cast nodes, 1x1 / grouped
+    convolutions as anonymous ``onnx::Conv_*``, every Conv + BatchNorm pair fused (no BN parameters left), the
+    pre-encode convolutions under the exporter's nested ``conv.0`` / ``conv.0.0`` scopes, one Linear through
+    Gemm(transB=1) and one through an explicit Transpose, norm gains still named with the ``_model.`` prefix."""
+    inits, nodes = [], []
+    cnt = [0]
+
+    def anon(kind, arr):
+        cnt[0] += 1
+        name = f"onnx::{kind}_{cnt[0]}"
+        inits.append(tensor_proto(name, np.ascontiguousarray(arr)))
+        return name
+
+    def scope(mod):
+        segs = mod.split(".")
+        out, i = [], 0
+        while i < len(segs):          # ModuleList children: "layers.0"; nested containers: "conv.0" / "conv.0.0"
+            if i + 1 < len(segs) and segs[i + 1].isdigit():
+                out.append(segs[i] + "." + segs[i + 1])
+                i += 2
+                while i < len(segs) and segs[i].isdigit():
+                    out.append(out[-1] + "." + segs[i])
+                    i += 1
+            else:
+                out.append(segs[i])
+                i += 1
+        return "/_model/" + "/".join(out)
+
+    done = set()
+    for k in PARAM_SHAPES:
+        if k in done:
+            continue
+        mod, leaf = k.rsplit(".", 1)
+        v = w[k]
+        if leaf in ("running_mean", "running_var") or (leaf in ("weight", "bias") and (mod + ".running_var") in w):
+            continue                                                      # BatchNorm: fused below
+        if leaf == "bias" and (mod + ".weight") in w:
+            continue                                                      # with its weight
+        if v.ndim == 1 or "_ln." in k:                                    # norm gains / LayerNorm: named
+            names = [mod + "." + r for r in ("weight", "bias") if (mod + "." + r) in w]
+            for n in names:
+                inits.append(tensor_proto("_model." + n, w[n].astype(np.float32)))
+                done.add(n)
+            op = "LayerNormalization" if "_ln." in k else "Mul"
+            nodes.append(node_proto(scope(mod) + "/" + op, op, ["x"] + ["_model." + n for n in names], [mod + "_out"]))
+            continue
+        b = w.get(mod + ".bias")
+        bn = mod.rsplit(".", 1)[0] + ".1." if mod.endswith(".0") else None
+        if mod.endswith("depthwise_conv.conv"):
+            bn = mod.rsplit(".", 2)[0] + ".batch_norm."
+        if bn and (bn + "running_var") in w:                              # Conv + BN fused
+            wf, bf = _fold_bn(w, mod + ".", bn)
+            wn, bnm = anon("Conv", wf), anon("Conv", bf)
+            nodes.append(node_proto(scope(mod) + "/Conv", "Conv", ["x", wn, bnm], [mod + "_out"]))
+        elif v.ndim == 3:                                                  # 1x1 / grouped Conv1d
+            ins = ["x", anon("Conv", v.astype(np.float16))] + ([anon("Conv", b.astype(np.float16))] if b is not None else [])
+            nodes.append(node_proto(scope(mod) + "/Conv", "Conv", ins, [mod + "_out"]))
+        elif k == "encoder.pre_encode.out.weight":                        # Gemm(transB=1), original orientation
+            nodes.append(node_proto(scope(mod) + "/Gemm", "Gemm", ["x", anon("Gemm", v.astype(np.float16))],
+                                    [mod + "_out"], {"transB": 1}))
+        elif k == "encoder.layers.5.self_attn.linear_out.weight":        # explicit Transpose then MatMul
+            t = anon("Transpose", v.astype(np.float16))
+            nodes.append(node_proto(scope(mod) + "/Transpose", "Transpose", [t], [mod + "_wt"], {"perm": [1, 0]}))
+            nodes.append(node_proto(scope(mod) + "/MatMul", "MatMul", ["x", mod + "_wt"], [mod + "_mm"]))
+        else:                                                              # Linear: folded [in, out] MatMul weight
+            nodes.append(node_proto(scope(mod) + "/MatMul", "MatMul", ["x", anon("MatMul", v.T.astype(np.float16))],
+                                    [mod + "_mm"]))
+        if b is not None and not (bn and (bn + "running_var") in w) and v.ndim == 2:
+            inits.append(tensor_proto(f"onnx::Cast_{mod}", b.astype(np.float32)))
+            nodes.append(node_proto(scope(mod) + "/Cast", "Cast", [f"onnx::Cast_{mod}"], [mod + "_b16"], {"to": 10}))
+            nodes.append(node_proto(scope(mod) + "/Add", "Add", [mod + "_mm", mod + "_b16"], [mod + "_out"]))
+    return model_proto(inits, nodes)
+
+
+def test_constant_folded_export_graph(tmp_path):
+    """ADVICE r2 / VERDICT r2 #5: the loader reads a model.onnx shaped like the reference's real export (see
+    export_like_graph): every parameter comes back -- square Linear weights in the right orientation (decided by
+    the consuming MatMul / Gemm / Transpose, not by shape), biases through Cast, fused Conv+BN as the fused conv
+    with an identity BatchNorm.  The step computed from the loaded weights equals the step from the checkpoint
+    (fp16-rounded, as the export stores it) up to the fusion's fp32 rounding."""
+    from tone_oracle import ToneOracle
+    w = {k: v.astype(np.float16).astype(np.float32) for k, v in synthetic_weights(3).items()}
+    p = tmp_path / "model.onnx"
+    p.write_bytes(export_like_graph(w))
+    got = load_onnx_weights(p)
+    assert list(got) == list(PARAM_SHAPES)
+    for k in ("encoder.layers.0.self_attn.linear_q.weight", "encoder.layers.9.self_attn.linear_v.weight",
+              "encoder.layers.5.self_attn.linear_out.weight", "encoder.layers.2.feed_forward2.linear2.weight",
+              "encoder.pre_encode.out.weight", "encoder.layers.3.conv.pointwise_conv2.weight",
+              "encoder.temportal_reduction.conv_pw.weight", "decoder.decoder_layers.0.bias",
+              "encoder.layers.14.norm_self_att.weight", "encoder.layers.15.self_attn.k_ln.bias"):
+        np.testing.assert_array_equal(got[k], w[k], err_msg=k)
+    np.testing.assert_array_equal(got["encoder.layers.4.conv.batch_norm.weight"], np.ones(384, np.float32))
+    rng = np.random.default_rng(1)
+    pcm = np.clip(rng.normal(0, 3000, (2, 2400)), -32768, 32767).astype(np.int32)
+    lp_ref, _ = ToneOracle(w).step(pcm)
+    lp_got, _ = ToneOracle(got).step(pcm)
+    assert np.abs(lp_got - lp_ref).max() < 2e-3
+
+
+def test_download_prefers_safetensors_then_onnx(monkeypatch):
+    """from_hugging_face asks the HF cache for model.safetensors first (every parameter by name) and falls back
+    to the reference's own artifact, model.onnx (tone/onnx_wrapper.py:60-63), when that fails."""
+    import huggingface_hub
+    from tone_amd.model import StreamingCTCModel
+    asked = []
+
+    def fake(repo, fname):
+        asked.append((repo, fname))
+        if fname == "model.safetensors":
+            raise FileNotFoundError(fname)
+        return "/cache/" + fname
+
+    monkeypatch.setattr(huggingface_hub, "hf_hub_download", fake)
+    assert StreamingCTCModel.download_from_hugging_face() == "/cache/model.onnx"
+    assert asked == [("t-tech/T-one", "model.safetensors"), ("t-tech/T-one", "model.onnx")]
