@@ -324,9 +324,15 @@ class StreamingCTCModel:
     def session(self) -> ToneSession:
         return self._sess
 
+    _MAX_IO_SETS = 4   # device I/O buffer sets kept for distinct batch sizes (least recently used evicted)
+
     def _io(self, b: int):
         torch = _torch()
-        if b not in self._buffers:
+        if b in self._buffers:
+            self._buffers[b] = self._buffers.pop(b)          # most recently used last
+        else:
+            while len(self._buffers) >= self._MAX_IO_SETS:
+                self._buffers.pop(next(iter(self._buffers)))
             dev = self._sess.dev
             self._buffers[b] = (
                 torch.empty((b, C.AUDIO_CHUNK_SAMPLES), dtype=torch.int32, device=dev),
