@@ -373,10 +373,7 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
 template <int T, bool OBF>
 static hipError_t launch_dwconv_t(const float* g, StateRef s, int layer, const float* w, const float* b, void* out,
                                   int B, hipStream_t st) {
-  static const int forced = [] {   // TONE_DWCONV_VARIANT (sweeps only): 0 = 384x2, 1 = 128x1, 2 = 384x1, 3 = 192x1
-    const char* e = std::getenv("TONE_DWCONV_VARIANT");
-    return e ? std::atoi(e) : -1;
-  }();
+  const int forced = knobs().dwconv_variant;   // TONE_DWCONV_VARIANT (sweeps only): 0 = 384x2, 1 = 128x1, 2 = 384x1, 3 = 192x1
   const int v = forced >= 0 ? forced : (B >= 1024 ? 3 : 1);   // profiles/r01_dwconv_sweep.txt
   if (v == 0)
     hipLaunchKernelGGL((dwconv_kernel<T, OBF, kD, 2>), dim3((B + 1) / 2, 1), dim3(kD), 0, st, g, s, layer, w, b, out, B);

@@ -418,209 +418,10 @@ hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale
 }
 
 // ---------------------------------------------------------------------------------------------
-// a3 conv2 in fp32 (split) mode: the slab kernel above with fp32 arithmetic done as exact 3-way bf16
-// splits (6 products per multiply-add; gemm_t.hip split3 explains the error bound).
-// Workgroup = (stream, half): output rows 5h .. 5h + 4 read input rows 15h .. 15h + 22, an fp32
-// slab of 1012 positions x 128 B (127 KiB) staged once by LDS-DMA.  The weights arrive pre-split and
-// pre-swizzled, one tap (3 planes x 64 channels x 32 bf16 = 12 KiB) per ring slot, double-buffered.
-// K order inside a tap is permuted so that a lane's 8 k-values are the 16-byte slab slots g and
-// g + 4 (channels 4g..4g+3 and 16+4g..16+4g+3): with the slab slot swizzle s ^ ((q >> 1) & 7) the
-// two ds_read_b128 of a 16-position tile are conflict-free for row-aligned tiles.  X is split in
-// registers (split3); 11 tiles of 16 positions cover the 170 positions.
-constexpr int kC3Rows = 5;                                        // output rows per workgroup
-constexpr int kC3InRows = kSub2Stride * (kC3Rows - 1) + kSub2Kt;  // 23
-constexpr int kC3In = kC3InRows * kSub1F;                         // 1012 input positions
-constexpr int kC3SlabPieces = (kC3In * 128 + 1023) / 1024;        // 127
-constexpr int kC3Slab = kC3SlabPieces * 256;                      // floats
-constexpr int kC3Tap = 3 * kSub2C * kSub1C / 2;                   // floats of one tap's planes (12 KiB)
-constexpr int kC3Pos = kC3Rows * kSub2F;                          // 170
-constexpr int kC3Tiles = (kC3Pos + 15) / 16;                      // 11
-static_assert(kC3Slab * 4 + 2 * kC3Tap * 4 + 2 * kSub2C * 4 <= 160 * 1024, "conv2_x3 LDS");
-
-// 400 ms (T = 13): three workgroups per stream (5 + 5 + 3 output rows); the last one's slab window
-// is clamped to the stream's 48 input rows and its positions past row 13 are not stored.
-// DBG (TONE_CONV2_DBG, ablations only): bit 0 taps not re-staged (every tap reads slot 0), bit 1 no
-// split, bit 2 no MFMA
-template <int NWV, int T, int DBG = 0>   // waves per workgroup (8: two per SIMD; 4: one per SIMD, 3 tiles each); frames
-__global__ void __launch_bounds__(NWV * 64) conv2_x3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2x,
-                                                       const float* __restrict__ scale, const float* __restrict__ shift,
-                                                       float* __restrict__ flat) {
-  constexpr int kParts = (T + kC3Rows - 1) / kC3Rows;
-  constexpr int kIn = (T == make_geom(3200).T ? make_geom(3200) : make_geom(2400)).sub2In;   // input rows per stream
-  constexpr int kC2PosT = T * kSub2F;
-  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) float lds[kC3Slab + 2 * kC3Tap + 2 * kSub2C];   // slab | ring | sc | sh
-  float* ring = lds + kC3Slab;
-  float* sc = ring + 2 * kC3Tap;
-  float* sh = sc + kSub2C;
-  const int b = blockIdx.x / kParts, half = blockIdx.x % kParts;
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rows = min(kC3Rows, T - half * kC3Rows), posT = rows * kSub2F;   // this part's output rows
-  const int in_left = (kIn - half * kSub2Stride * kC3Rows) * kSub1F;          // input positions left in the stream
-  const float* xb = x2 + ((int64_t)b * kIn * kSub1F + half * kSub2Stride * kC3Rows * kSub1F) * kSub1C;
-  if (tid < kSub2C) {
-    sc[tid] = scale[tid];
-    sh[tid] = shift[tid];
-  }
-  __syncthreads();                                        // before any LDS-DMA is in flight
-
-  auto stage_tap = [&](int j) {                           // 12 one-KiB pieces, contiguous in w2x
-    for (int pc = wid; pc < 12; pc += NWV) {
-      const uint16_t* src = w2x + (int64_t)j * (2 * kC3Tap) + pc * 512 + lane * 8;
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, ring + (j & 1) * kC3Tap + pc * 256, 16, 0, 0);
-#else
-      (void)src;
-#endif
-    }
-  };
-  for (int pc = wid; pc < kC3SlabPieces; pc += NWV) {     // the slab, once: lane -> (q, swizzled slot)
-    const int L = pc * 64 + lane, q = L >> 3, s = (L & 7) ^ ((q >> 1) & 7);
-    const float* src = xb + min(q, min(kC3In, in_left) - 1) * kSub1C + s * 4;
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src, lds + pc * 256, 16, 0, 0);
-#else
-    (void)src;
-#endif
-  }
-  stage_tap(0);
-
-  // wave w: position tiles w and w + 8 (when < 11) x all 4 channel tiles, so each slab fragment is
-  // split once per wave and feeds 24 MFMAs (the split VALU, 4 cycles per wave64 op, would otherwise
-  // bound the kernel); per SIMD (waves w, w + 4) 3/3/3/2 tiles
-  constexpr int KT = (kC3Tiles + NWV - 1) / NWV, KU = kC3Tiles / NWV;   // tiles per wave: max, unconditional
-  const int n = lane & 15, g = lane >> 4;
-  const int ntile = wid + NWV * (KT - 1) < kC3Tiles ? KT : KT - 1;   // wave-uniform
-  int qb[KT];
-#pragma unroll
-  for (int k = 0; k < KT; ++k) {
-    const int p = min((wid + NWV * k) * 16 + n, kC3Pos - 1);
-    qb[k] = kSub2Stride * (p / kSub2F) * kSub1F + p % kSub2F;
-  }
-  int wofs[4];
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int wrow = 16 * ct + n;
-    wofs[ct] = wrow * 16 + ((g ^ c2_swz(wrow)) << 2);
-  }
-  f32x4 acc[KT][4];
-#pragma unroll
-  for (int k = 0; k < KT; ++k)
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) acc[k][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int j = 0; j < kC2Taps; ++j) {
-    if (!(DBG & 1) || j == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      barrier_lds_c2();                                   // tap j (and the slab) landed; slot (j+1)&1 free
-      if (j + 1 < kC2Taps && !(DBG & 1)) stage_tap(j + 1);
-    }
-    const float* wr = ring + ((DBG & 1) ? 0 : (j & 1)) * kC3Tap;
-    bf16x8 w[3][4];
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) w[pl][ct] = *reinterpret_cast<const bf16x8*>(wr + pl * 1024 + wofs[ct]);
-    const int kt = j / kSub2Kf, kf = j - kt * kSub2Kf, toff = kt * kSub1F + kf;
-#pragma unroll
-    for (int k = 0; k < KT; ++k) {
-      if (k < KU || k < ntile) {
-        const int q = qb[k] + toff, h = (q >> 1) & 7;
-        const f32x4 a = *reinterpret_cast<const f32x4*>(lds + q * 32 + ((g ^ h) << 2));
-        const f32x4 c = *reinterpret_cast<const f32x4*>(lds + q * 32 + (((g + 4) ^ h) << 2));
-        bf16x8 x0, x1, xl;
-        const float x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-        if constexpr ((DBG & 2) != 0) {
-          x0 = __builtin_bit_cast(bf16x8, a);
-          x1 = __builtin_bit_cast(bf16x8, c);
-          xl = x0;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const __bf16 h0 = (__bf16)x[e];
-            const float r1 = x[e] - (float)h0;
-            const __bf16 h1 = (__bf16)r1;
-            x0[e] = h0;
-            x1[e] = h1;
-            xl[e] = (__bf16)(r1 - (float)h1);
-          }
-        }
-        if constexpr ((DBG & 4) != 0) {
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct)
-            acc[k][ct][0] += __builtin_bit_cast(f32x4, x0).x + __builtin_bit_cast(f32x4, x1).y + __builtin_bit_cast(f32x4, xl).z +
-                             __builtin_bit_cast(f32x4, w[0][ct]).x + __builtin_bit_cast(f32x4, w[1][ct]).y + __builtin_bit_cast(f32x4, w[2][ct]).z;
-          continue;
-        }
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          f32x4 t = acc[k][ct];
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2][ct], x0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1][ct], x1, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], xl, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1][ct], x0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], x1, t, 0, 0, 0);
-          acc[k][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0][ct], x0, t, 0, 0, 0);
-        }
-      }
-    }
-  }
-  // epilogue: D[channel][position]; lane: position tile 16 + n, channels 16 ct + 4 g + r
-#pragma unroll
-  for (int k = 0; k < KT; ++k) {
-    if (k >= ntile) break;
-    const int p = (wid + NWV * k) * 16 + n;
-    if (p >= posT) continue;
-    float* dst = flat + ((int64_t)b * kC2PosT + half * kC3Pos + p) * kSub2C;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int ch = 16 * ct + 4 * g;
-      float4 y;
-      y.x = silu_f(fmaf(acc[k][ct][0], sc[ch], sh[ch]));
-      y.y = silu_f(fmaf(acc[k][ct][1], sc[ch + 1], sh[ch + 1]));
-      y.z = silu_f(fmaf(acc[k][ct][2], sc[ch + 2], sh[ch + 2]));
-      y.w = silu_f(fmaf(acc[k][ct][3], sc[ch + 3], sh[ch + 3]));
-      *reinterpret_cast<float4*>(dst + ch) = y;
-    }
-  }
-}
-
-hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, const float* shift, void* flat, int B,
-                           int T, hipStream_t st) {
-  static const int nwv = [] {   // TONE_CONV2_WAVES (sweeps only): 8 (default) or 4
-    const char* e = std::getenv("TONE_CONV2_WAVES");
-    return e ? std::atoi(e) : 8;
-  }();
-  const float* xs = static_cast<const float*>(x2);
-  const uint16_t* ws = static_cast<const uint16_t*>(w2x);
-  float* fl = static_cast<float*>(flat);
-  if (T == 13) hipLaunchKernelGGL((conv2_x3_kernel<8, 13>), dim3(3 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
-  else if (T != kT) return hipErrorInvalidValue;
-  else if (nwv == 4) hipLaunchKernelGGL((conv2_x3_kernel<4, kT>), dim3(2 * B), dim3(256), 0, st, xs, ws, scale, shift, fl);
-  else {
-    static const int dbg = [] {   // TONE_CONV2_DBG (ablations only)
-      const char* e = std::getenv("TONE_CONV2_DBG");
-      return e ? std::atoi(e) : 0;
-    }();
-    switch (dbg) {
-      case 1: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 1>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
-      case 2: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 2>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
-      case 3: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 3>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
-      case 4: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 4>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
-      case 5: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 5>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
-      case 7: hipLaunchKernelGGL((conv2_x3_kernel<8, kT, 7>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl); break;
-      default: hipLaunchKernelGGL((conv2_x3_kernel<8, kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
-    }
-  }
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// a3 conv2 in fp32 (split) mode, input split once per kernel row ("p3").  conv2_x3 above splits every
-// slab fragment again for each of the 121 taps (21x redundant VALU, profiles/r02_conv2_x3_ablate.txt:
-// the split costs ~58 us of 283 at B = 256).  Here the loop runs kernel row kt outer, kernel column kf
-// inner: the 5 input rows that kt reads (3 r + kt for output rows r) are split ONCE into three bf16
+// a3 conv2 in fp32 (split) mode, input split once per kernel row ("p3").  The round-1 kernel (conv2_x3, since
+// removed) split every slab fragment again for each of the 121 taps (21x redundant VALU,
+// profiles/r02_conv2_x3_ablate.txt: the split cost ~58 us of 283 at B = 256).  Here the loop runs kernel row kt
+// outer, kernel column kf inner: the 5 input rows that kt reads (3 r + kt for output rows r) are split ONCE into three bf16
 // planes in LDS, and the 11 taps of that row read their X fragments from the planes directly (three
 // ds_read_b128, no VALU).  Per workgroup (stream, part of 5 output rows), 8 waves:
 //   * W taps (pre-split, natural channel order) stream through a 3-slot ring, issued by waves 0-3
@@ -825,8 +626,7 @@ hipError_t launch_conv2_p3(const void* x2, const void* w2p, const float* scale, 
   const float* xs = static_cast<const float*>(x2);
   const uint16_t* ws = static_cast<const uint16_t*>(w2p);
   float* fl = static_cast<float*>(flat);
-  const char* e = std::getenv("TONE_C2_PRIO");   // read per launch: in-process A/B (scripts/ab_env.py)
-  const int prio = e ? std::atoi(e) : 0;
+  const int prio = knobs().c2_prio;
   if (T == 13) hipLaunchKernelGGL((conv2_p3_kernel<13>), dim3(3 * B), dim3(512), 0, st, xs, ws, scale, shift, fl, prio);
   else if (T == kT) hipLaunchKernelGGL((conv2_p3_kernel<kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl, prio);
   else return hipErrorInvalidValue;
@@ -842,21 +642,6 @@ void conv2_p3_pack(const uint16_t* planes, uint16_t* w2p) {
         for (int ci = 0; ci < kSub1C; ++ci)
           w2p[(((int64_t)tap * 3 + pl) * kSub2C + c) * kSub1C + (((ci >> 3) ^ p3_swz(c)) << 3) + (ci & 7)] =
               planes[(((int64_t)pl * kSub2C + c) * kC2Taps + tap) * kSub1C + ci];
-}
-
-// Host-side layout of w2x: [tap][plane][c 64][32 bf16], the k order of a row permuted (k' = 8g + e
-// holds input channel 4g + e for e < 4, 16 + 4g + e - 4 otherwise) and its 16-byte slots swizzled
-// (slot g stored at g ^ c2_swz(c)).  planes[pl][c][tap][ci] are the three bf16 split terms.
-void conv2_x3_pack(const uint16_t* planes, uint16_t* w2x) {
-  for (int tap = 0; tap < kC2Taps; ++tap)
-    for (int pl = 0; pl < 3; ++pl)
-      for (int c = 0; c < kSub2C; ++c)
-        for (int kk = 0; kk < kSub1C; ++kk) {
-          const int g = kk >> 3, e = kk & 7, ci = e < 4 ? 4 * g + e : 16 + 4 * g + (e - 4);
-          const int slot = g ^ c2_swz(c);
-          w2x[(((int64_t)tap * 3 + pl) * kSub2C + c) * kSub1C + slot * 8 + e] =
-              planes[(((int64_t)pl * kSub2C + c) * kC2Taps + tap) * kSub1C + ci];
-        }
 }
 
 }  // namespace tone

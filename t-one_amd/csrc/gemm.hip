@@ -686,143 +686,6 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
   gemm_epilogue<TL, EPI, CBF, false>(p, acc, rden, m0, n0, wm, wn, lane);
 }
 
-// Persistent bf16 GEMM (large M): one workgroup per CU walks its tiles with ONE LDS-DMA ring that
-// runs across tile boundaries, so the first K-steps of tile i+1 are in flight while tile i's
-// epilogue (LDS-staged, its own LDS region) drains -- no per-tile prologue bubble and no idle
-// memory pipe during stores.  Tiles are dealt XCD-contiguously: the workgroups of one XCD walk
-// neighbouring tiles together, so an A row-block is fetched into that XCD's L2 once.
-// Plain row-major A only (no rpg / conv2 gathers), no split-K.
-template <class TL, int EPI, bool CBF>
-__global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_persist_kernel(GemmArgs p) {
-  constexpr int BM = TL::BM, BN = TL::BN, WM = TL::WM, WN = TL::WN;
-  constexpr int kNWaves = WM * WN, NT = kNWaves * 64;
-  constexpr int BK = 64;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int A_I = BM / 8 / kNWaves, W_I = BN / 8 / kNWaves;
-  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
-  constexpr int BNO = PAIRED ? BN / 2 : BN;
-  static_assert(A_I >= 1 && W_I >= 1, "tile/wave mismatch");
-  static_assert(EPI == EPI_STORE || EPI == EPI_RESID || PAIRED, "persistent GEMM: STORE/RESID/SWIGLU/GLU");
-  constexpr int kStageElems = (BM + BN) * BK;
-  // ONE LDS object (a second __shared__ array can make hipcc fence every ds_read behind the DMAs)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kStageElems + 2 * BM * BNO + 2 * BM];
-  float* Cs = reinterpret_cast<float*>(lds + 2 * kStageElems);
-  float* rden = Cs + BM * BNO;
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int ntn = p.N / BN, ntm = (p.M + BM - 1) / BM, ntiles = ntm * ntn;
-  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
-  const int q = (ntiles + 7) >> 3, tbeg = xcd * q, tend = min(ntiles, tbeg + q);
-  const int ntile_mine = (tend - tbeg - jb + nxb - 1) / nxb;    // tiles tbeg+jb, +nxb, ...
-  if (ntile_mine <= 0) return;
-  const int nk = p.K / BK;
-  const int G = ntile_mine * nk;                                 // K-steps of all my tiles
-  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
-  const uint16_t* __restrict__ W = static_cast<const uint16_t*>(p.W);
-  const int lrow8 = lane >> 3, lslot = lane & 7;
-
-  auto tile_mn = [&](int g, int& m0, int& n0) {
-    const int t = tbeg + jb + (g / nk) * nxb;
-    m0 = (t / ntn) * BM;
-    n0 = (t % ntn) * BN;
-  };
-  auto stage = [&](int buf, int g) {
-    int m0, n0;
-    tile_mn(g, m0, n0);
-    const int k0 = (g % nk) * BK;
-    uint16_t* base = lds + buf * kStageElems;
-    (void)base;
-#pragma unroll
-    for (int i = 0; i < A_I; ++i) {
-      const int row = 8 * (wid + i * kNWaves) + lrow8;
-      const int gm = min(m0 + row, p.M - 1);
-      const uint16_t* src = A + (int64_t)gm * p.lda + k0 + ((lslot ^ (row & 7)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + (8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
-#else
-      (void)src;
-#endif
-    }
-#pragma unroll
-    for (int i = 0; i < W_I; ++i) {
-      const int row = 8 * (wid + i * kNWaves) + lrow8;
-      const uint16_t* src = W + (int64_t)(n0 + row) * p.K + k0 + ((lslot ^ (row & 7)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + (BM + 8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
-#else
-      (void)src;
-#endif
-    }
-  };
-
-  f32x16 acc[TM][TN];
-  float ss[TM];
-  auto zero = [&]() {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      ss[i] = 0.f;
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    }
-  };
-  zero();
-  const bool want_ss = p.rowscale && wn == 0;
-  const int lr = lane & 31, lh = lane >> 5;
-
-  stage(0, 0);
-  for (int g = 0; g < G; ++g) {
-    wait_vmcnt<0>();
-    lds_barrier();
-    if (g + 1 < G) stage((g + 1) & 1, g + 1);
-    const uint16_t* base = lds + (g & 1) * kStageElems;
-    bf16x8 a[BK / 16][TM], b[BK / 16][TN];
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int slot = ks * 2 + lh;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WTM + i * 32 + lr;
-        a[ks][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((slot ^ (row & 7)) << 3));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * WTN + j * 32 + lr;
-        b[ks][j] = *reinterpret_cast<const bf16x8*>(base + (BM + row) * BK + ((slot ^ (row & 7)) << 3));
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) ss[i] = sumsq_bf16x8(a[ks][i], ss[i]);
-    }
-    if (g % nk == nk - 1) {   // tile finished: epilogue while the next tile's first K-step loads
-      int m0, n0;
-      tile_mn(g, m0, n0);
-      if (p.rowscale) {
-        if (want_ss) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            const float v = ss[i] + __shfl_xor(ss[i], 32, 64);
-            if (lh == 0) rden[wm * WTM + i * 32 + lr] = sqrtf(v) * p.inv_sqrt_k + kRmsEps;
-          }
-        }
-        lds_barrier();
-      }
-      gemm_epilogue_lds<TL, EPI, CBF, false>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
-      zero();
-    }
-  }
-}
-
 // Split-K combine: fixed-order sum of the partials, then the STORE/RESID epilogue.
 template <int EPI, bool CBF>
 __global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmArgs p, int nsplit) {
@@ -937,24 +800,6 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   constexpr int kTarget = 512;
   // large batches: the persistent transposed-orientation kernels (gemm_t.hip, tools/gemm_bench sweep)
   const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
-  // FFN up (SwiGLU): the pipelined 16x16x32 kernel with 16-byte stores; inside the real step (scripts/ab_route.py,
-  // profiles/r02_ab_route.jsonl) it beats gemm_t by 3 % on FFN up, while pw1 (fp32 GLU output) stays on gemm_t
-  // (gemm_t.hip gemm_p_kernel; FFN up M = 20480: 72.9 vs 82.1 us, pw1 20.1 vs 22.5 us for gemm_t,
-  // scripts/gp_sweep.sh, profiles/r02_gemm_p_sweep.jsonl)
-  // TONE_GEMM_P (experiments): bit 0 SwiGLU, bit 1 GLU on gemm_p; low nibble of bits 4.. = gemm_p variant
-  // Default now off: the in-step A/B of this tree (scripts/ab_env.py, profiles/r02_ab_ffnup.jsonl) has the 2-stage
-  // transposed kernel ahead at every batch (B = 2048: 6.38 vs 6.74 ms/step; B = 512: 2.57 vs 2.86)
-  const char* route_env = getenv("TONE_GEMM_P");
-  const int route = route_env ? atoi(route_env) : 0;
-  // default variant 7: 2D XCD blocks with 4 n-groups where the tiles divide evenly (87.6-90.9 vs 88-93 us at
-  // M = 20480, 166 vs 182 at 40960; profiles/r02_gemm_p_xcd.txt), else the XCD-contiguous order
-  const int pv0 = (route >> 4) & 15;
-  const int pv = (pv0 == 0 && (a.N / 256) % 4 == 0 && ((a.M + 255) / 256) % 2 == 0) ? 7 : pv0;
-  // TONE_SWIGLU_T = 1 + gemm_t variant (experiments): FFN up on the transposed 2-stage kernel at every M
-  const char* swt = getenv("TONE_SWIGLU_T");
-  if (epi == EPI_SWIGLU && swt && atoi(swt) > 0 && a.N % 256 == 0) return gemm_t(a, epi, atoi(swt) - 1, st);
-  if (epi == EPI_SWIGLU && (route & 1) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
-  if (epi == EPI_GLU && (route & 2) && a.N % 256 == 0 && t256 >= 96) return gemm_p(a, epi, pv, st);
   // FFN up: 256 x 256 tiles once there are ~180 of them (M >= 3840 at N = 3072), 256 W x 128 X rows below that
   // down to ~200 tiles (M = 2560: 14.5 vs 20.2 us; tools/gemm_bench, profiles/r02_ffnup_route.jsonl)
   if (epi == EPI_SWIGLU && a.N % 256 == 0 && t256 >= 180) return gemm_t(a, epi, 0, st);
@@ -987,39 +832,6 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   return launch_glds_epi<Tile<32, 128, 1, 2>>(a, epi, 1, st);
 }
 
-static int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-template <class TL, int EPI, bool CBF>
-static hipError_t launch_persist(const GemmArgs& a, int per_cu, hipStream_t st) {
-  if (a.N % TL::BN || a.K % 64 || a.rpg) return hipErrorInvalidValue;
-  const int tiles = ((a.M + TL::BM - 1) / TL::BM) * (a.N / TL::BN);
-  int grid = num_cus() * per_cu;
-  const int need = ((tiles + 7) / 8) * 8;
-  if (grid > need) grid = need;
-  grid = (grid + 7) / 8 * 8;
-  hipLaunchKernelGGL((gemm_persist_kernel<TL, EPI, CBF>), dim3(grid), dim3(TL::WM * TL::WN * 64), 0, st, a);
-  return hipGetLastError();
-}
-
-template <class TL>
-static hipError_t launch_persist_epi(const GemmArgs& a, int epi, int per_cu, hipStream_t st) {
-  switch (epi) {
-    case EPI_STORE: return a.c_bf16 ? launch_persist<TL, EPI_STORE, true>(a, per_cu, st) : launch_persist<TL, EPI_STORE, false>(a, per_cu, st);
-    case EPI_RESID: return launch_persist<TL, EPI_RESID, false>(a, per_cu, st);
-    case EPI_SWIGLU: return a.c_bf16 ? launch_persist<TL, EPI_SWIGLU, true>(a, per_cu, st) : launch_persist<TL, EPI_SWIGLU, false>(a, per_cu, st);
-    case EPI_GLU: return a.c_bf16 ? launch_persist<TL, EPI_GLU, true>(a, per_cu, st) : launch_persist<TL, EPI_GLU, false>(a, per_cu, st);
-    default: return hipErrorInvalidValue;
-  }
-}
-
 // Fixed bf16 tile/stage variants (tools/gemm_bench.hip), bypassing the size heuristics.
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st) {
   switch (variant) {
@@ -1033,10 +845,6 @@ hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit
     case 7: return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, nsplit, st);
     case 8: return launch_glds_epi<Tile<64, 128, 2, 2>, 3>(a, epi, nsplit, st);
     case 9: return launch_glds_epi<Tile<64, 128, 2, 2>, 4>(a, epi, nsplit, st);
-    case 10: return launch_persist_epi<Tile<128, 128, 2, 2>>(a, epi, 1, st);
-    case 11: return launch_persist_epi<Tile<64, 128, 2, 2>>(a, epi, 1, st);
-    case 12: return launch_persist_epi<Tile<64, 128, 2, 2>>(a, epi, 2, st);
-    case 13: return launch_persist_epi<Tile<128, 128, 2, 2>>(a, epi, 2, st);
     case 14: return launch_glds_epi<Tile<128, 128, 4, 2>, 2>(a, epi, nsplit, st);
     default: return hipErrorInvalidValue;
   }
@@ -1073,8 +881,7 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   if (bf16 && a.a_bf16) {
     if (a.K % 64 != 0 || a.N % 128 != 0 || a.M <= 0 || (epi == EPI_RESID && a.c_bf16)) return hipErrorInvalidValue;
     GemmArgs b = a;
-    const char* e = std::getenv("TONE_PRIO_BF16");   // read per call: in-process A/B (scripts/ab_env.py)
-    b.prio = e && std::atoi(e) == 1;
+    b.prio = knobs().prio_bf16;
     return gemm_bf16(b, epi, st);
   }
   if (!bf16 && a.W3 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
@@ -1086,13 +893,6 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     // step the ring kernel is slower (profiles/r02_r3_sweep.jsonl)
     if (epi == EPI_STORE && a.N == 768 && a.M >= 4096 && a.W && !a.rowscale)
       return gemm_r3(a, epi, a.M >= 8192 ? 0 : 1, st);
-    // ping-pong schedule (gemm_pp) for the FFN up-projection; TONE_PP = 1 + variant, 0 = off
-    static const int pp = [] {
-      const char* e = std::getenv("TONE_PP");
-      return e ? std::atoi(e) : 0;
-    }();
-    if (pp > 0 && a.W3b && epi == EPI_SWIGLU && a.N % 256 == 0 && (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200)
-      return gemm_pp(a, epi, pp - 1, st);
     if (epi == EPI_SWIGLU && a.N % 256 == 0)
       return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200 ? 7 : 6, st);
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
@@ -1134,18 +934,12 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
 }
 
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st, const void* w2x, int chunk, const void* w2p) {
+                      bool bf16, hipStream_t st, int chunk, const void* w2p) {
   const Geom geo = make_geom(chunk);
   // per-stream LDS slab kernel (frontend.hip): the 300 ms slab (38 rows, 107 KB) fits, 400 ms (48) does not
   if (bf16 && geo.T == kT) return launch_conv2_bf16(x2, w, scale, shift, flat, B, st);
-  // fp32 split mode (frontend.hip): input rows split once per kernel row (conv2_p3); TONE_CONV2_KERNEL=x3
-  // selects the per-tap split kernel (A/B measurements)
-  static const bool use_x3 = [] {
-    const char* e = std::getenv("TONE_CONV2_KERNEL");
-    return e && std::string(e) == "x3";
-  }();
-  if (w2p && !use_x3) return launch_conv2_p3(x2, w2p, scale, shift, flat, B, geo.T, st);
-  if (w2x) return launch_conv2_x3(x2, w2x, scale, shift, flat, B, geo.T, st);
+  // fp32 split mode (frontend.hip): input rows split once per kernel row (conv2_p3)
+  if (w2p) return launch_conv2_p3(x2, w2p, scale, shift, flat, B, geo.T, st);
   GemmArgs a{};
   a.A = x2;
   a.W = w;

@@ -397,10 +397,7 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
 
 hipError_t gemm_mx(const MxArgs& a0, int epi, hipStream_t st) {
   MxArgs a = a0;
-  {
-    const char* e = std::getenv("TONE_PRIO_MX");   // read per call: in-process A/B (scripts/ab_env.py)
-    a.prio = e && std::atoi(e) == 1;
-  }
+  a.prio = knobs().prio_mx;
   // 128 W rows per tile: the 256-row tile needs 96 fragment VGPRs per wave at 32 bytes per lane and
   // spills at two waves per SIMD
   if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || (a.ldc % 8) || a.N % 128) return hipErrorInvalidValue;

@@ -177,276 +177,6 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_t_kernel(GemmArgs p
 }
 
 // ---------------------------------------------------------------------------------------------
-// gemm_p: the large-batch bf16 projections with a deeper LDS-DMA pipeline (BASELINE config 3).
-// Same transposed orientation, tile (256 W rows x 256 X rows, BK = 64) and persistent XCD-contiguous
-// tile order as gemm_t_kernel, but
-//   * v_mfma_f32_16x16x32_bf16 (the chip holds a higher clock on it than on 32x32x16 at equal
-//     cycles per FLOP, MI355X_MICROARCH.md DVFS item 7); wave tile 128 (n) x 64 (m) = 8 x 4 tiles;
-//   * each K-tile's stage is four 16 KiB quarters (W rows 0-127 | 128-255 | X rows 0-127 | 128-255)
-//     and a wave reads ALL of its K-tile fragments in the first two of the K-tile's four MFMA phases,
-//     so the stage is free after the first barrier: the quarters of K-tile t+2 go out during phases
-//     2-3 of t and 0-1 of t+1, and a counted vmcnt(4) at the end of K-tile t retires K-tile t+1
-//     while two quarters of t+2 stay in flight across the barrier (never vmcnt(0) in the loop);
-//   * two barriers per K-tile (reads done / next K-tile landed), raw s_barrier (no vmcnt drain);
-//   * the folded-RMSNorm row scale is computed by every wave from its own X fragments (no LDS).
-// Phases of one K-tile (each 16 MFMAs): (n 0-63, m 0-31), (n 0-63, m 32-63), (n 64-127, m 32-63),
-// (n 64-127, m 0-31) of the wave tile.  LDS: 2 x 64 KiB stages + the bias vector.
-template <int EPI, bool RS, bool PRIO, int DBG = 0, int STK = 0, int ROT = 0>
-__global__ void __launch_bounds__(512) gemm_p_kernel(GemmArgs p) {
-  constexpr int BK = 64, QB = 128 * BK, STG = 4 * QB;
-  constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
-  static_assert(EPI == EPI_STORE || EPI == EPI_RESID || PAIRED, "STORE/RESID/SWIGLU/GLU");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STG + 2 * kBiasMax];
-  float* sbias = reinterpret_cast<float*>(lds + 2 * STG);
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wid >> 2, wm = wid & 3, l15 = lane & 15, lg = lane >> 4, cs = (l15 >> 1) & 7;
-  const int ntn = p.N >> 8, ntm = (p.M + 255) >> 8, ntiles = ntn * ntm;
-  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
-  const int q = (ntiles + 7) >> 3, tbeg = xcd * q, tend = min(ntiles, tbeg + q);
-  const int nmine = (tbeg + jb < tend) ? (tend - tbeg - jb + nxb - 1) / nxb : 0;
-  if (nmine <= 0) return;                                       // workgroup-uniform
-  const int nk = p.K / BK, G = nmine * nk;
-  const uint16_t* __restrict__ X = static_cast<const uint16_t*>(p.A);
-  const uint16_t* __restrict__ W = static_cast<const uint16_t*>(p.W);
-  if constexpr (PRIO) {   // static priority for the younger half (MI355X_MICROARCH.md, two waves per SIMD item 4)
-    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
-  }
-
-  for (int i = tid; i < p.N; i += 512) sbias[i] = p.bias ? p.bias[i] : 0.f;
-  __syncthreads();                                              // no DMA in flight yet
-
-  auto tile_of = [&](int u, int& m0, int& n0) {
-    if (p.xcd_a) {   // 2D XCD blocks (GemmArgs::xcd_a): XCD x owns n-group x % a and m-group x / a
-      const int a = p.xcd_a, npg = ntn / a, li = jb + (u / nk) * nxb;
-      n0 = ((xcd % a) * npg + li % npg) << 8;
-      m0 = ((xcd / a) * (ntm / (8 / a)) + li / npg) << 8;
-      return;
-    }
-    const int t = tbeg + jb + (u / nk) * nxb;
-    m0 = (t / ntn) << 8;
-    n0 = (t % ntn) << 8;
-  };
-  // quarter j of K-tile u: W rows 128j.. (j < 2) or X rows 128(j-2).. (j >= 2); 2 pieces of 8 rows x
-  // 128 B per wave, slot ^= (row >> 1) & 7 on the source address (conflict-free fragment reads)
-  auto issue = [&](int u, int j) {
-    if constexpr ((DBG & 4) != 0) return;                       // microbenchmark: no staging
-    int m0, n0;
-    tile_of(u, m0, n0);
-    // ROT: each tile walks its K-tiles from a different start (the tile index mod nk), so the CUs that
-    // stream the same X rows / W rows at the same time ask for different 128-byte lines
-    const int rot = ROT ? (tbeg + jb + (u / nk) * nxb) % nk : 0;
-    const int k0 = ((u % nk + rot) % nk) * BK;
-    uint16_t* dst = lds + (u & 1) * STG + j * QB;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int piece = 2 * wid + h, row = piece * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      const uint16_t* src = (j < 2) ? W + (int64_t)(n0 + 128 * j + row) * p.K + k0 + 8 * c
-                                    : X + (int64_t)min(m0 + 128 * (j - 2) + row, p.M - 1) * p.lda + k0 + 8 * c;
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, dst + piece * 8 * BK, 16, 0, 0);
-#else
-      (void)src;
-      (void)dst;
-#endif
-    }
-  };
-  // 16x16x32 fragment: row 16 * tile + (lane & 15) of the wave's W quarter / X rows, k-chunk 4s + lane/16
-  const uint16_t* wq = lds + wn * QB;
-  const uint16_t* xq = lds + (2 + (wm >> 1)) * QB + (wm & 1) * 64 * BK;
-  auto rd = [&](const uint16_t* qb, int buf, int tile, int s) {
-    return *reinterpret_cast<const bf16x8*>(qb + buf * STG + (16 * tile + l15) * BK + 8 * ((4 * s + lg) ^ cs));
-  };
-
-  f32x4 acc[8][4];
-  float ss[4];
-  auto mm = [&](const bf16x8& a, const bf16x8& b, f32x4& c) {
-    if constexpr ((DBG & 2) != 0) {                             // microbenchmark: fragments read, no MFMA
-      asm volatile("" ::"v"(a), "v"(b));
-      return;
-    }
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  };
-  auto zero = [&]() {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ss[j] = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-
-  auto st4 = [&](void* base, int64_t off, const float (&v)[4], bool ok, bool bf) {
-    if (bf) {
-      const uint2 w = {pk2(v[0], v[1]), pk2(v[2], v[3])};
-      if (ok) *reinterpret_cast<uint2*>(static_cast<uint16_t*>(base) + off) = w;
-    } else {
-      const f32x4 w = {v[0], v[1], v[2], v[3]};
-      if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(base) + off) = w;
-    }
-  };
-  auto epilogue = [&](int u) {
-    int m0, n0;
-    tile_of(u, m0, n0);
-    const float* sb = sbias + n0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float inv = 1.0f;
-      if constexpr (RS) {
-        float t = ss[j] + __shfl_xor(ss[j], 16, 64);
-        t += __shfl_xor(t, 32, 64);
-        inv = 1.0f / (sqrtf(t) * p.inv_sqrt_k + kRmsEps);
-      }
-      const int m = m0 + wm * 64 + 16 * j + l15;
-      const bool ok = m < p.M;
-      const int64_t mrow = min(m, p.M - 1);
-      if constexpr (PAIRED) {
-        uint32_t pa[2][2];
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const int ig = (ii & 1) + 4 * (ii >> 1);                 // g tiles 0,1,4,5; u tile ig + 2
-          const int nl = wn * 128 + 64 * (ii >> 1) + 16 * (ii & 1) + 4 * lg;
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float g = fmaf(acc[ig][j][r], inv, sb[nl + r]);
-            const float uu = fmaf(acc[ig + 2][j][r], inv, sb[nl + 32 + r]);
-            if (p.c_bf16) o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * uu : g * fast_sigmoid(uu);
-            else o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * uu : g * sigmoid_f(uu);
-          }
-          if (p.c_bf16) {
-            // tiles ii (cols 0-15 of the 32-col block) and ii + 1 (cols 16-31): v_permlane16_swap of the
-            // packed runs gives every lane 8 contiguous bf16 -> one 16-byte store per lane per tile pair
-            // (lane group lg stores cols 16 (lg & 1) + 8 (lg >> 1) of the block)
-            pa[ii & 1][0] = pk2(o[0], o[1]);
-            pa[ii & 1][1] = pk2(o[2], o[3]);
-            if (ii & 1) {
-              const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
-              const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
-              const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
-              const int col = (n0 >> 1) + wn * 64 + 32 * (ii >> 1) + 16 * (lg & 1) + 8 * (lg >> 1);
-              uint16_t* dst = static_cast<uint16_t*>(p.C) + mrow * p.ldc + col;
-              if (ok) {
-                if constexpr (STK == 1) __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(dst));
-                else if constexpr (STK == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(w) : "memory");
-                else *reinterpret_cast<u32x4*>(dst) = w;
-              }
-            }
-          } else {
-            const int col = (n0 >> 1) + wn * 64 + 32 * (ii >> 1) + 16 * (ii & 1) + 4 * lg;
-            st4(p.C, mrow * p.ldc + col, o, ok, false);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int nl = wn * 128 + 16 * i + 4 * lg;
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[i][j][r], inv, sb[nl + r]);
-          if constexpr (EPI == EPI_RESID) {
-            const f32x4 rr = *reinterpret_cast<const f32x4*>(p.R + mrow * p.ldr + n0 + nl);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = rr[r] + p.alpha * v[r];
-            st4(p.C, mrow * p.ldc + n0 + nl, v, ok, false);
-          } else {
-            st4(p.C, mrow * p.ldc + n0 + nl, v, ok, p.c_bf16);
-          }
-          if (p.C2) st4(p.C2, mrow * p.ldc + n0 + nl, v, ok, true);   // bf16 shadow of an fp32 C
-        }
-      }
-    }
-  };
-
-  zero();
-  // prologue: K-tile 0 whole, quarters 0-1 of K-tile 1
-  issue(0, 0);
-  issue(0, 1);
-  issue(0, 2);
-  issue(0, 3);
-  if (G > 1) {
-    issue(1, 0);
-    issue(1, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  barrier_lds();
-  for (int t = 0; t < G; ++t) {
-    const int buf = t & 1;
-    bf16x8 xf[4][2], wa[4][2], wb[4][2];
-    // phase 0: every X fragment of the K-tile + W rows 0-63 of the wave tile
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) xf[j][s2] = rd(xq, buf, j, s2);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) wa[i][s2] = rd(wq, buf, i, s2);
-    if (t + 1 < G) issue(t + 1, 2);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          mm(wa[i][s2], xf[j][s2], acc[i][j]);
-    if constexpr (RS) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ss[j] = sumsq8(xf[j][1], sumsq8(xf[j][0], ss[j]));
-    }
-    // phase 1: W rows 64-127 of the wave tile (the stage's last reads)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) wb[i][s2] = rd(wq, buf, 4 + i, s2);
-    if (t + 1 < G) issue(t + 1, 3);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 2; j < 4; ++j)
-          mm(wa[i][s2], xf[j][s2], acc[i][j]);
-    barrier_lds();                                              // every wave's reads of stage buf done
-    // phase 2
-    if (t + 2 < G) issue(t + 2, 0);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 2; j < 4; ++j)
-          mm(wb[i][s2], xf[j][s2], acc[4 + i][j]);
-    // phase 3
-    if (t + 2 < G) issue(t + 2, 1);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          mm(wb[i][s2], xf[j][s2], acc[4 + i][j]);
-    if (t + 2 < G) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // K-tile t+1 landed, t+2 q0-1 in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier_lds();                                              // ... for every wave
-    if (t % nk == nk - 1) {
-      if constexpr ((DBG & 1) == 0) {
-        epilogue(t);
-      } else {   // keep every accumulator live (no epilogue, MFMAs not dead)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-        asm volatile("" ::"v"(ss[0]), "v"(ss[1]), "v"(ss[2]), "v"(ss[3]));
-      }
-      zero();
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Two workgroups per CU: 4 waves (2 n x 2 m), tile BNW x BMX (256 x 128: wave tile 128 x 64),
 // BK = 32 (64-byte LDS rows, swizzle slot ^= (row >> 2) & 3, conflict-free for the 32x32x16
 // fragment reads), three LDS-DMA stages (two K-steps in flight).  One tile per workgroup; the two
@@ -768,9 +498,7 @@ struct XT {
 
 // XS: X arrives pre-split (3 bf16 planes written by its producer, GemmArgs::a_plane) and is staged
 // like W -- no split VALU in the loop; otherwise X is fp32 and split from its LDS fragment.
-// HL: only the upper half of the waves (wid >= NW / 2) issues the LDS-DMA, twice the pieces each, so each
-// SIMD pairs a wave stalled in DMA issue with one that keeps its MFMAs going.
-template <class TL, int EPI, bool RS, bool XS, bool HL = false>
+template <class TL, int EPI, bool RS, bool XS>
 __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(GemmArgs p) {
   constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, WK = TL::WK, S = TL::S;
   constexpr int NW = WN * WM * WK, NT = NW * 64;
@@ -780,7 +508,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   constexpr int GROUP = 3 * WPL + (XS ? 3 * XPL : BMX * 32);    // floats of one wave group's slice
   constexpr int STAGE = WK * GROUP;
   constexpr int WPC = 3 * BNW / 16, XPC = XS ? 3 * BMX / 16 : BMX / 8;   // 1 KiB DMA pieces per group
-  constexpr int NL = HL ? NW / 2 : NW;                          // waves issuing the LDS-DMA
+  constexpr int NL = NW;                                        // waves issuing the LDS-DMA
   constexpr int PIECES = WK * (WPC + XPC), IPW = PIECES / NL;
   static_assert(PIECES % NL == 0 && IPW >= 1, "DMA pieces per wave");
   static_assert(TI >= 1 && TJ >= 1 && WN >= TJ, "wave tile / row-scale ownership");
@@ -835,10 +563,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   auto stage = [&](int buf, int kt) {
     float* base = lds + buf * STAGE;
     (void)base;
-    if (HL && wid < NW / 2) return;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-      const int piece = (HL ? wid - NW / 2 : wid) + i * NL;     // wave-uniform
+      const int piece = wid + i * NL;                           // wave-uniform
       const int g = piece / (WPC + XPC), pr = piece % (WPC + XPC);
       const int kb = kofs + (kt * WK + g) * 32;
       const void* src;
@@ -1026,10 +753,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
 // its LDS-DMA issue rate, not by L2 misses.
 template <class TL>
 int x3_xcd_split(const GemmArgs& a) {
-  static const int off = [] {
-    const char* e = std::getenv("TONE_X3_XCD");
-    return !(e && std::atoi(e) == 1);
-  }();
+  const bool off = !knobs().x3_xcd;
   const int ntn = a.N / TL::BNW, ntm = (a.M + TL::BMX - 1) / TL::BMX;
   if (off || a.k_split || (ntn & 7) == 0 || a.M % TL::BMX) return 0;
   const double wb = 6.0 * a.N * a.K, xb = (a.a_plane ? 6.0 : 4.0) * a.M * a.K;
@@ -1047,29 +771,11 @@ template <class TL, int EPI>
 hipError_t launch_x3(const GemmArgs& a0, hipStream_t st) {
   GemmArgs a = a0;
   a.xcd_a = x3_xcd_split<TL>(a0);
-  {
-    // static priority for waves NW/2.. (default; TONE_X3_PRIO=0 turns it off, read per launch for in-process A/B):
-    // fp32 B = 256 step 3.616 -> 3.583 ms, FFN down 897 -> 871 us (scripts/ab_env.py, profiles/r02_ab_x3_prio.jsonl)
-    const char* e = std::getenv("TONE_X3_PRIO");
-    if (!(e && std::atoi(e) == 0)) a.dbg |= 64;
-  }
+  // static priority for waves NW/2.. (default; TONE_X3_PRIO=0 turns it off): fp32 B = 256 step 3.616 -> 3.583 ms,
+  // FFN down 897 -> 871 us (profiles/r02_ab_x3_prio.jsonl)
+  if (knobs().x3_prio) a.dbg |= 64;
   const dim3 tiles((a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX), a.k_split ? a.K / a.k_split : 1);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
-  // TONE_X3_HL=1: half the waves issue the LDS-DMA (A/B only: 10-40 % slower on every B = 256 shape --
-  // the fill rate scales with the number of issuing waves, tools/dma_bench.hip)
-  static const int hl = [] {
-    const char* e = std::getenv("TONE_X3_HL");
-    return e ? std::atoi(e) : 0;
-  }();
-  constexpr int kNW = TL::WN * TL::WM * TL::WK;
-  constexpr int kPieces = TL::WK * (3 * TL::BNW / 16 + TL::BMX / 8);
-  if constexpr (kNW >= 4 && kPieces % (kNW / 2) == 0) {
-    if (hl && !a.a_plane) {
-      if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, false, true>), tiles, block, 0, st, a);
-      else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, false, true>), tiles, block, 0, st, a);
-      return hipGetLastError();
-    }
-  }
   if (a.a_plane) {
     if (a.rowscale) hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, true, true>), tiles, block, 0, st, a);
     else hipLaunchKernelGGL((gemm_x3_kernel<TL, EPI, false, true>), tiles, block, 0, st, a);
@@ -1494,72 +1200,6 @@ hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st) {
     case 1: return launch_f32t_epi<FT<128, 64, 2, 2, 2>>(a, epi, st);
     case 2: return launch_f32t_epi<FT<64, 64, 2, 2, 1>>(a, epi, st);
     case 3: return launch_f32t_epi<FT<64, 128, 2, 2, 2>>(a, epi, st);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// Tile variants: 0 = 256x256 (waves 2x4), 1 = 128x256 (2x4), 2 = 256x128 (2x4), 3 = 128x128 (2x4)
-template <int EPI, bool PRIO, int STK = 0, int ROT = 0>
-hipError_t launch_p(const GemmArgs& a, hipStream_t st) {
-  const int ntiles = (a.N / 256) * ((a.M + 255) / 256);
-  int grid = num_cus_t();
-  const int need = ((ntiles + 7) / 8) * 8;
-  if (grid > need) grid = need;
-  grid = (grid + 7) / 8 * 8;
-  if constexpr (STK != 0 || ROT != 0) {
-    if (a.rowscale) hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 0, STK, ROT>), dim3(grid), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((gemm_p_kernel<EPI, false, PRIO, 0, STK, ROT>), dim3(grid), dim3(512), 0, st, a);
-    return hipGetLastError();
-  }
-  if constexpr (EPI == EPI_SWIGLU && !PRIO) {   // microbenchmark ablations (tools/gemm_bench, dbg bits)
-    switch (a.dbg & 7) {
-      case 1: hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 1>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 2: hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 2>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 4: hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 4>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 5: hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 5>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 6: hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 6>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 3: hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 3>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 7: hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO, 7>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      default: break;
-    }
-  }
-  if (a.rowscale) hipLaunchKernelGGL((gemm_p_kernel<EPI, true, PRIO>), dim3(grid), dim3(512), 0, st, a);
-  else hipLaunchKernelGGL((gemm_p_kernel<EPI, false, PRIO>), dim3(grid), dim3(512), 0, st, a);
-  return hipGetLastError();
-}
-
-template <bool PRIO, int STK = 0, int ROT = 0>
-hipError_t launch_p_epi(const GemmArgs& a, int epi, hipStream_t st) {
-  if (!a.a_bf16 || a.N % 256 || a.K % 64 || a.N > kBiasMax || a.rpg || a.M <= 0 || a.c_plane || a.c2_plane ||
-      (a.ldc % 4) || (a.lda % 8))
-    return hipErrorInvalidValue;
-  switch (epi) {
-    case EPI_STORE: return launch_p<EPI_STORE, PRIO>(a, st);
-    case EPI_RESID: return a.c_bf16 ? hipErrorInvalidValue : launch_p<EPI_RESID, PRIO>(a, st);
-    case EPI_SWIGLU: return launch_p<EPI_SWIGLU, PRIO, STK, ROT>(a, st);
-    case EPI_GLU: return launch_p<EPI_GLU, PRIO, STK, ROT>(a, st);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// variant 0: gemm_p_kernel; 1: the same with static priority for waves 4-7; 2 / 3: paired epilogues with
-// non-temporal / sc1 (write-through, L2-dropping) 16-byte stores
-hipError_t gemm_p(const GemmArgs& a0, int epi, int variant, hipStream_t st) {
-  GemmArgs a = a0;
-  if (variant >= 6 && variant <= 8) {   // 2D XCD blocks, a = 2 / 4 / 8 n-groups (tiles must divide evenly)
-    const int sa = variant == 6 ? 2 : variant == 7 ? 4 : 8;
-    const int ntn = a.N / 256, ntm = (a.M + 255) / 256;
-    if (ntn % sa || ntm % (8 / sa)) return hipErrorInvalidValue;
-    a.xcd_a = sa;
-    variant = 0;
-  }
-  switch (variant) {
-    case 0: return launch_p_epi<false>(a, epi, st);
-    case 1: return launch_p_epi<true>(a, epi, st);
-    case 2: return launch_p_epi<false, 1>(a, epi, st);
-    case 3: return launch_p_epi<false, 2>(a, epi, st);
-    case 4: return launch_p_epi<false, 0, 1>(a, epi, st);   // K-tile rotation per tile
-    case 5: return launch_p_epi<false, 1, 1>(a, epi, st);
     default: return hipErrorInvalidValue;
   }
 }

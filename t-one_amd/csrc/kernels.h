@@ -9,6 +9,19 @@
 
 namespace tone {
 
+// Experiment switches, read from the environment ONCE per process (the first call; A/B runs compare separate
+// processes).  Defaults are the measured best; none of them changes the arithmetic.
+struct Knobs {
+  int prio_bf16;       // TONE_PRIO_BF16=1: static priority for waves 4-7 in the bf16 LDS-DMA GEMMs (default off)
+  int prio_mx;         // TONE_PRIO_MX=1: the same in the MXFP8 GEMMs (default off)
+  int x3_prio;         // TONE_X3_PRIO=0: no static priority in gemm_x3 (default on)
+  int x3_xcd;          // TONE_X3_XCD=1: 2D XCD tile blocks in gemm_x3 (default off)
+  int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand
+  int dwconv_variant;  // TONE_DWCONV_VARIANT: force a dwconv block shape (-1 = by batch)
+  int c2_prio;         // TONE_C2_PRIO: static priority role in conv2_p3 (default 0)
+};
+const Knobs& knobs();
+
 enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GLU = 3, EPI_CONV2 = 4, EPI_POWER = 5, EPI_LOGMEL = 6 };
 
 struct GemmArgs {
@@ -46,7 +59,6 @@ struct GemmArgs {
   int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
   int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
   int prio;           // bf16 kernels: static priority for the second half of the waves (set by gemm(), TONE_PRIO_BF16)
-  const uint16_t* W3b; // fp32 mode: the same planes K16-blocked, [3][K/16][N][16] (gemm_pp), or nullptr
   int xcd_a;          // gemm_x3: XCD x owns the 2D tile block (n-group x % a, m-group x / a) of an a x (8 / a)
                       // split (set by the launcher; 0 = the default order)
 };
@@ -86,16 +98,11 @@ hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // persistent transposed-orientation bf16 GEMM (gemm_t.hip); variant = tile shape, see there
 hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
-// pipelined 256x256 bf16 GEMM on v_mfma_f32_16x16x32_bf16 (gemm_t.hip gemm_p_kernel); variant: 0, 1 = + static priority
-hipError_t gemm_p(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3
 hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // the same with the K range split over nsplit workgroups (partials in a.ws, fixed-order combine; gemm.hip)
-// the same arithmetic, ping-pong schedule (two wave groups alternating LDS/VALU and MFMA segments;
-// gemm_t.hip gemm_pp_kernel); needs a.W3b
-hipError_t gemm_pp(const GemmArgs& a, int epi, int variant, hipStream_t st);
 hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // the same arithmetic with fp32 W and X streamed through a K-tile ring (gemm_t.hip gemm_r3_kernel); needs a.W fp32
 hipError_t gemm_r3(const GemmArgs& a, int epi, int variant, hipStream_t st);
@@ -104,18 +111,12 @@ hipError_t gemm_r3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // [B][38][44][32] input (one 32-deep K-step = one (kt,kf) tap), W [64][121*32] tap-major,
 // epilogue SiLU(acc*scale + shift) -> flat [B*10][34*64] (f-major, channel-minor).
 hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const float* shift, void* flat, int B,
-                      bool bf16, hipStream_t st, const void* w2x = nullptr, int chunk = kChunk, const void* w2p = nullptr);
+                      bool bf16, hipStream_t st, int chunk = kChunk, const void* w2p = nullptr);
 
 // a3 conv2 in bf16 mode, one workgroup per stream over an LDS-resident input slab (frontend.hip);
 // x2 bf16 [B][38][44][32], w2c bf16 [64][3904] tap-major, flat bf16 [B*10][34*64]
 hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale, const float* shift, void* flat, int B,
                              hipStream_t st);
-// a3 conv2 in fp32 (split) mode: two workgroups per stream over fp32 LDS slabs, exact 3-way bf16
-// splits on the bf16 MFMA (frontend.hip); x2 fp32 [B][38][44][32], flat fp32 [B*10][34*64]
-hipError_t launch_conv2_x3(const void* x2, const void* w2x, const float* scale, const float* shift, void* flat, int B,
-                           int T, hipStream_t st);
-// host: pack the split planes [3][64][121][32] (bf16 bits) into the conv2_x3 tap-major layout
-void conv2_x3_pack(const uint16_t* planes, uint16_t* w2x);
 // a3 conv2 in fp32 (split) mode, input rows split once per kernel row (frontend.hip conv2_p3_kernel);
 // w2p from conv2_p3_pack
 hipError_t launch_conv2_p3(const void* x2, const void* w2p, const float* scale, const float* shift, void* flat, int B,

@@ -22,6 +22,29 @@
 
 using namespace tone;
 
+namespace tone {
+
+const Knobs& knobs() {
+  static const Knobs k = [] {
+    auto env = [](const char* n, int dflt) {
+      const char* e = std::getenv(n);
+      return e && *e ? std::atoi(e) : dflt;
+    };
+    Knobs r;
+    r.prio_bf16 = env("TONE_PRIO_BF16", 0) == 1;
+    r.prio_mx = env("TONE_PRIO_MX", 0) == 1;
+    r.x3_prio = env("TONE_X3_PRIO", 1) != 0;
+    r.x3_xcd = env("TONE_X3_XCD", 0) == 1;
+    r.fp8_normq = env("TONE_FP8_NORMQ", 1) != 0;
+    r.dwconv_variant = env("TONE_DWCONV_VARIANT", -1);
+    r.c2_prio = env("TONE_C2_PRIO", 0);
+    return r;
+  }();
+  return k;
+}
+
+}  // namespace tone
+
 namespace {
 
 thread_local std::string g_err;
@@ -94,15 +117,13 @@ struct tone_session {
   float *pre_norm, *w1, *scale1, *shift1, *scale2, *shift2, *out_norm;
   void* w1t = nullptr;   // bf16 mode: conv1 weights [kt 11][c 32][kf 32] (kf >= 21 zero)
   void* w2c;
-  uint16_t* w2x = nullptr;   // fp32 (split) mode: conv2 split planes packed for conv2_x3 (frontend.hip)
-  uint16_t* w2p = nullptr;   // ... and for conv2_p3 (natural channel order)
+  uint16_t* w2p = nullptr;   // fp32 (split) mode: conv2 split planes packed for conv2_p3 (frontend.hip)
   void* wsub_out;
   float *wred, *bred, *bred_pw;
   void* wred_pw;
   float *whead, *bhead;
   LayerW L[16];
   std::map<const void*, const uint16_t*> w3;   // fp32 (split) mode: GEMM weight -> its bf16 planes
-  std::map<const void*, const uint16_t*> w3b;  // ... and their K16-blocked copy (encoder weights, gemm_pp)
 
   // activations
   float *wave, *power, *feats, *rA, *rB, *qkv, *kvp, *g, *probs;
@@ -227,7 +248,7 @@ int upload_mx(tone_session* s, MxW* out, const std::vector<float>& v, int N, int
 // GEMM weight in the session's precision (fp32, or bf16 bits).  fp32 (split) mode also uploads the
 // exact three-term bf16 split [3][N][K] (w = w0 + w1 + w2, each term the bf16 rounding of what the
 // previous ones leave) that gemm_x3 reads.
-int upload_w(tone_session* s, void** out, const std::vector<float>& v, int K = 0) {
+int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
   if (!bfmode(s)) {
     float* p;
     int rc = upload(s, &p, v);
@@ -248,20 +269,6 @@ int upload_w(tone_session* s, void** out, const std::vector<float>& v, int K = 0
     if (rc) return rc;
     HIP_TRY(hipMemcpy(d, pl.data(), pl.size() * 2, hipMemcpyHostToDevice));
     s->w3[p] = d;
-    static const bool pp = std::getenv("TONE_PP") && std::atoi(std::getenv("TONE_PP")) > 0;
-    if (pp && K > 0 && K % 16 == 0 && n % K == 0) {   // K16-blocked copy [3][K/16][N][16] for gemm_pp (TONE_PP)
-      const size_t N = n / K;
-      std::vector<uint16_t> bl(3 * n);
-      for (int q = 0; q < 3; ++q)
-        for (int kb = 0; kb < K / 16; ++kb)
-          for (size_t r = 0; r < N; ++r)
-            std::memcpy(&bl[(((size_t)q * (K / 16) + kb) * N + r) * 16], &pl[(size_t)q * n + r * K + kb * 16], 32);
-      uint16_t* db;
-      rc = dalloc(s, &db, bl.size());
-      if (rc) return rc;
-      HIP_TRY(hipMemcpy(db, bl.data(), bl.size() * 2, hipMemcpyHostToDevice));
-      s->w3b[p] = db;
-    }
     return TONE_OK;
   }
   std::vector<uint16_t> hb(v.size());
@@ -416,8 +423,6 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   if (s->precision == TONE_PRECISION_FP32) {
     auto it = s->w3.find(W);
     a.W3 = it == s->w3.end() ? nullptr : it->second;
-    auto ib = s->w3b.find(W);
-    a.W3b = ib == s->w3b.end() ? nullptr : ib->second;
   }
   LAUNCH(fam, gemm(a, epi, bf, st));
   return TONE_OK;
@@ -479,17 +484,13 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   if (s->debug_stop == 0) return TONE_OK;
   LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B, geo.chunk,
                              st));
-  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, s->w2x, geo.chunk, s->w2p));
+  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, geo.chunk, s->w2p));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * geo.T, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
   // fp8 mode: the norms that feed a layer's FFN1 directly also emit its MXFP8 operand (no quant_mx launch)
   // (TONE_FP8_NORMQ=0 keeps the separate quant_mx launches; the operands are bit-identical either way,
   // tests/test_gpu_parity.py::test_fp8_norm_quant_fusion_matches_quant_mx; 0.6-1 % per step, profiles/r02_fp8_normq_ab.txt)
-  static const bool normq = [] {
-    const char* e = std::getenv("TONE_FP8_NORMQ");
-    return !(e && std::atoi(e) == 0);
-  }();
-  const bool f8n = f8 && normq;
+  const bool f8n = f8 && knobs().fp8_normq;
   bool q8_fresh = f8n;
   LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st, f8n ? s->a8 : nullptr, s->a8s, s->inv8));
   if (s->debug_stop == 1) {
@@ -710,9 +711,6 @@ int finalize_weights(tone_session* s) {
         pl[n + i] = m;
         pl[2 * n + i] = f2bf(r1 - bf2f(m));
       }
-      conv2_x3_pack(pl.data(), px.data());
-      CALL(dalloc(s, &s->w2x, px.size()));
-      HIP_TRY(hipMemcpy(s->w2x, px.data(), px.size() * 2, hipMemcpyHostToDevice));
       conv2_p3_pack(pl.data(), px.data());
       CALL(dalloc(s, &s->w2p, px.size()));
       HIP_TRY(hipMemcpy(s->w2p, px.data(), px.size() * 2, hipMemcpyHostToDevice));
@@ -759,9 +757,9 @@ int finalize_weights(tone_session* s) {
           b13[64 * q + r] = (*b1)[src];
           b13[64 * q + 32 + r] = (*bv)[src];
         }
-      CALL(upload_w(s, &lw.w13[f], w13, D));
+      CALL(upload_w(s, &lw.w13[f], w13));
       CALL(upload(s, &lw.b13[f], b13));
-      CALL(upload_w(s, &lw.w2[f], *w2, kDff));
+      CALL(upload_w(s, &lw.w2[f], *w2));
       if (s->precision == TONE_PRECISION_FP8) {
         CALL(upload_mx(s, &lw.mx13[f], w13, 2 * kDff, D));
         CALL(upload_mx(s, &lw.mx2[f], *w2, D, kDff));
@@ -802,7 +800,7 @@ int finalize_weights(tone_session* s) {
           bqkv[m * D + n] = (*bias[src])[n];
         }
       }
-      CALL(upload_w(s, &lw.wqkv, wqkv, D));
+      CALL(upload_w(s, &lw.wqkv, wqkv));
       if (s->precision == TONE_PRECISION_FP8) CALL(upload_mx(s, &lw.mxqkv, wqkv, nb * D, D));
       CALL(upload(s, &lw.bqkv, bqkv));
     } else {
@@ -811,9 +809,9 @@ int finalize_weights(tone_session* s) {
       std::memcpy(wkv.data() + (size_t)D * D, wv->data(), (size_t)D * D * 4);
       std::memcpy(bkv.data(), bk->data(), D * 4);
       std::memcpy(bkv.data() + D, bv->data(), D * 4);
-      CALL(upload_w(s, &lw.wq, *wq, D));
+      CALL(upload_w(s, &lw.wq, *wq));
       CALL(upload(s, &lw.bq, *bq));
-      CALL(upload_w(s, &lw.wkv, wkv, D));
+      CALL(upload_w(s, &lw.wkv, wkv));
       if (s->precision == TONE_PRECISION_FP8) {
         CALL(upload_mx(s, &lw.mxq, *wq, D, D));
         CALL(upload_mx(s, &lw.mxkv, wkv, 2 * D, D));
@@ -821,7 +819,7 @@ int finalize_weights(tone_session* s) {
       CALL(upload(s, &lw.bkv, bkv));
       CALL(upload(s, &lw.norm_att, *natt));
     }
-    CALL(upload_w(s, &lw.wo, *wo, D));
+    CALL(upload_w(s, &lw.wo, *wo));
     CALL(upload(s, &lw.bo, *bo));
 
     const std::string c = p + "conv.";
@@ -847,7 +845,7 @@ int finalize_weights(tone_session* s) {
         bp[64 * q + r] = (*pb1)[src];
         bp[64 * q + 32 + r] = (*pb1)[D + src];
       }
-    CALL(upload_w(s, &lw.wpw1, wp, D));
+    CALL(upload_w(s, &lw.wpw1, wp));
     CALL(upload(s, &lw.bpw1, bp));
     std::vector<float> wd((size_t)D * kConvK), bd(D);
     for (int ch = 0; ch < D; ++ch) {
@@ -857,7 +855,7 @@ int finalize_weights(tone_session* s) {
     }
     CALL(upload(s, &lw.wdw, wd));
     CALL(upload(s, &lw.bdw, bd));
-    CALL(upload_w(s, &lw.wpw2, *pw2, D));
+    CALL(upload_w(s, &lw.wpw2, *pw2));
     CALL(upload(s, &lw.bpw2, *pb2));
     CALL(upload(s, &lw.norm_out, *nout));
   }
@@ -945,7 +943,9 @@ int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp,
         auto lru = s->graphs.begin();
         for (auto g = s->graphs.begin(); g != s->graphs.end(); ++g)
           if (g->second.last_use < lru->second.last_use) lru = g;
-        HIP_TRY(hipStreamSynchronize(st));   // the evicted graph may still be in flight on this stream
+        // the evicted executable may still be in flight on any stream it was launched on (the key does not
+        // include the stream): wait for the device, which only happens on an eviction
+        HIP_TRY(hipDeviceSynchronize());
         (void)hipGraphExecDestroy(lru->second.exec);
         s->graphs.erase(lru);
       }

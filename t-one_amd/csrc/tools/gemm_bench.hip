@@ -210,7 +210,6 @@ int main(int argc, char** argv) {
   const int fullf32 = getenv("FULLF32") ? atoi(getenv("FULLF32")) : 0;
   float *Af, *Wf;
   uint16_t* W3;   // the three bf16 planes of Wf (gemm_x3)
-  uint16_t* W3b;  // the same K16-blocked (gemm_pp; PP=1 maps variants 50-59 onto gemm_pp 0-9)
   uint16_t* A3;   // the three bf16 planes of Af (gemm_x3 with a pre-split A, variants 60-65)
   {
     std::vector<float> fa(hA.size()), fw(hW.size());
@@ -232,15 +231,6 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(Af, fa.data(), fa.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(Wf, fw.data(), fw.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(W3, w3.data(), w3.size() * 2, hipMemcpyHostToDevice));
-    // the same planes K16-blocked, [3][K/16][N][16] (gemm_pp)
-    std::vector<uint16_t> w3b(w3.size());
-    for (int pl = 0; pl < 3; ++pl)
-      for (int kb = 0; kb < K / 16; ++kb)
-        for (int n = 0; n < N; ++n)
-          for (int e = 0; e < 16; ++e)
-            w3b[(((size_t)pl * (K / 16) + kb) * N + n) * 16 + e] = w3[(size_t)pl * N * K + (size_t)n * K + kb * 16 + e];
-    CK(hipMalloc(&W3b, w3b.size() * 2));
-    CK(hipMemcpy(W3b, w3b.data(), w3b.size() * 2, hipMemcpyHostToDevice));
     std::vector<uint16_t> a3(3 * fa.size());
     for (size_t i = 0; i < fa.size(); ++i) {
       const uint16_t h = to_bf16(fa[i]);
@@ -256,7 +246,6 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(bias, hb.data(), N * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(R, hR.data(), hR.size() * 4, hipMemcpyHostToDevice));
   const int rowscale = getenv("ROWSCALE") ? atoi(getenv("ROWSCALE")) : 0;
-  const int pp = getenv("PP") ? atoi(getenv("PP")) : 0;
   if (fullf32) hipLaunchKernelGGL(ref64_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, Af, Wf, bias, R, ref, M, N, K, epi, rowscale);
   else hipLaunchKernelGGL(ref_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, A, W, bias, R, ref, M, N, K, epi, rowscale);
   CK(hipDeviceSynchronize());
@@ -290,8 +279,6 @@ int main(int argc, char** argv) {
     const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 50) || (v >= 50 && v < 90);
     // -2: gemm() fp32 routing with W planes, -3: without, -4: with W and A planes
     a.W3 = (vv == -2 || vv == -4 || (v >= 50 && v < 90)) ? W3 : nullptr;
-    a.W3b = (vv == -2 || vv == -4 || (v >= 50 && v < 60)) ? W3b : nullptr;
-    if (pp && v >= 50 && v < 60 && getenv("PPXCD")) a.dbg |= 16;
     a.a_plane = (vv == -4 || (v >= 60 && v < 70)) ? (int64_t)M * K : 0;
     a.A = a.a_plane ? (const void*)A3 : f32 ? (const void*)Af : (const void*)A;
     a.W = f32 ? (const void*)Wf : (const void*)W;
@@ -299,10 +286,8 @@ int main(int argc, char** argv) {
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
       return v < 0 ? gemm(a, epi, !f32, 0)
-             : v >= 90 ? gemm_p(a, epi, v - 90, 0)
              : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
-             : (v >= 50 && v < 60 && pp) ? gemm_pp(a, epi, v - 50, 0)
              : (v >= 50 && nsplit > 1) ? gemm_x3_splitk(a, epi, v - 50, nsplit, 0)
              : v >= 50 ? gemm_x3(a, epi, v - 50, 0)
              : v >= 40 ? gemm_r3(a, epi, v - 40, 0)        // 40-49: fp32 W and X, K-tile ring

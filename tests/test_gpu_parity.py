@@ -501,7 +501,7 @@ def test_low_precision_example_audio_greedy_decode(weights, oracle, prec):
 @pytest.mark.gpu
 def test_fp32_pre_encode_split_vs_mfma(weights, oracle):
     """fp32 front end + subsampling from a carried state, split mode (conv2 on the two-slab
-    conv2_x3 kernel, 6 bf16 products per MAC) and exact-fp32-MFMA mode (implicit GEMM) vs the
+    conv2_p3 kernel, 6 bf16 products per MAC) and exact-fp32-MFMA mode (implicit GEMM) vs the
     oracle's pre-encode output: both at fp32 level, the split no worse than 2x the fp32 MFMA."""
     _gpu()
     from tone_amd.model import ToneSession
