@@ -320,6 +320,45 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
     return res
 
 
+def dropin_latency_b1(dev_index: int, calls: int = 200) -> dict:
+    """Per-call latency of the numpy drop-in at B = 1, the reference pipeline's call pattern
+    (tone/pipeline.py:146): StreamingCTCModel.forward with host chunk + host state in and host logprobs + next
+    state out (the 440 KB state crosses PCIe both ways every call, as with ORT's CUDA execution provider), next
+    to the device-resident step (ToneSession.run, graph replay) of the same batch."""
+    from tone_amd.model import StreamingCTCModel
+    sess = ToneSession(replica_weights(None, None), device=dev_index, precision="fp32", max_batch=1)
+    model = StreamingCTCModel(sess)
+    pcm = synthetic_pcm(np.random.default_rng(7), 1, 8)[:, :, :, None]      # (chunks, 1, 2400, 1)
+    st = None
+    for i in range(5):
+        _, st = model.forward(pcm[i % 8], st)
+    ts = []
+    for i in range(calls):
+        t0 = time.perf_counter()
+        _, st = model.forward(pcm[i % 8], st)
+        ts.append(time.perf_counter() - t0)
+    dev = sess.dev
+    sig = torch.from_numpy(pcm[0, :, :, 0]).to(dev)
+    s_in = torch.zeros((1, C.STATE_SIZE), dtype=torch.float16, device=dev)
+    s_out, lp = torch.empty_like(s_in), torch.empty((1, sess.frames, C.VOCAB), dtype=torch.float32, device=dev)
+    for _ in range(5):
+        sess.run(sig, s_in, lp, s_out)
+    torch.cuda.synchronize()
+    td = []
+    for i in range(calls):
+        t0 = time.perf_counter()
+        sess.run(sig, s_in if i % 2 == 0 else s_out, lp, s_out if i % 2 == 0 else s_in)
+        torch.cuda.synchronize()
+        td.append(time.perf_counter() - t0)
+    sess.close()
+    return {"batch": 1, "calls": calls, "dropin_numpy_median_ms": round(float(np.median(ts)) * 1e3, 3),
+            "dropin_numpy_p99_ms": round(float(np.percentile(ts, 99)) * 1e3, 3),
+            "device_step_median_ms": round(float(np.median(td)) * 1e3, 3),
+            "device_step_p99_ms": round(float(np.percentile(td, 99)) * 1e3, 3),
+            "what": "StreamingCTCModel.forward at B = 1 (host I/O, as pipeline.py:146 calls it) vs ToneSession.run "
+                    "with device-resident I/O (graph replay + sync), fp32"}
+
+
 def workload_line(name, res, n_streams, steps, dtype, chunk=C.AUDIO_CHUNK_SAMPLES, **extra):
     dt = res["elapsed"] / steps
     chunk_ms = chunk * 1000.0 / C.SAMPLE_RATE
@@ -418,6 +457,7 @@ def main() -> None:
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_s > 0:
         cpu = cpu_baseline(args.cpu_baseline_s)
+    lat = dropin_latency_b1(local) if rank == 0 and world == 1 and args.alt else None
 
     if rank == 0:
         if args.global_batch:
@@ -451,6 +491,7 @@ def main() -> None:
             "rtf": round(ms_step / 300.0, 5),
             "roofline": res["roofline"],
             "cpu_baseline": cpu,
+            "latency_b1": lat,
             "alt_workloads": alts,
         }
         print(json.dumps(out), flush=True)

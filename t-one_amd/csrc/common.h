@@ -92,6 +92,8 @@ __device__ __forceinline__ int mx_exp(float amax) {
   const int e = (int)((__float_as_uint(amax) >> 23) & 0xff);   // biased exponent of amax (0 for 0/subnormal)
   return max(0, min(254, e - 8));
 }
+// clamp to e4m3's finite range (+-448) keeping a NaN a NaN (fminf / fmaxf alone would turn it into -448)
+__device__ __forceinline__ float sat_e4m3(float v) { return v != v ? v : fminf(fmaxf(v, -448.f), 448.f); }
 __device__ __forceinline__ float exp2i(int ebiased) {
   return __uint_as_float((uint32_t)(254 - ebiased) << 23);
 }

@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, con
 #pragma unroll
       for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
       const int e = mx_exp(am);
-      const float a = fminf(fmaxf(vb * exp2i(e), -448.f), 448.f);
+      const float a = sat_e4m3(vb * exp2i(e));
       q8[(int64_t)row * kD + lane + 64 * i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(a, 0.f, 0, false) & 0xff);
       if ((lane & 31) == 0) s8[(int64_t)row * (kD / 32) + 2 * i + (lane >> 5)] = (uint8_t)e;
     }

@@ -20,6 +20,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace tone {
 namespace {
@@ -38,11 +39,12 @@ __device__ __forceinline__ float fsig(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
 
-// v / 2^(E - 127) clamped to e4m3's range, two values packed into the low / high half of `w`
+// v / 2^(E - 127) clamped to e4m3's range, two values packed into the low / high half of `w`; a NaN stays a
+// NaN (the conversion encodes it as e4m3 NaN) instead of being clamped to a finite value
 template <bool HI>
 __device__ __forceinline__ uint32_t cvt_pk(float a, float b, float inv, uint32_t w) {
-  a = fminf(fmaxf(a * inv, -448.f), 448.f);
-  b = fminf(fmaxf(b * inv, -448.f), 448.f);
+  a = sat_e4m3(a * inv);
+  b = sat_e4m3(b * inv);
   return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, (int)w, HI);
 }
 // 8 floats -> 8 e4m3 bytes with the block's inverse scale
@@ -393,7 +395,216 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// X-stationary MXFP8 GEMM for K = 384 (FFN up + SwiGLU -> MXFP8 h, q|k|v STORE), the fp8 form of gemm_xs
+// (gemm_xs.hip): each wave keeps its 32 X rows x 384 e4m3 in registers (48 VGPRs) with their E8M0 scales and
+// row factors, W tiles of 64 rows x 384 B (24 KiB) stream through a 4-deep LDS ring (chunk c of row r at slot
+// c ^ ((r >> 1) & 7), the mx_swz map on 384-byte rows: conflict-free for both ds_read_b128 of a fragment), the
+// W scales of the whole matrix sit in LDS for the launch, and the accumulators are double-buffered so tile
+// t - 1's epilogue (SwiGLU + the MXFP8 quantization of h: one 64-row W tile = one 32-column MX block of h)
+// runs under tile t's MFMAs.  2 x 64 x 256 x 384 FLOP per 24 KiB of W: 524 FLOP per staged byte.
+constexpr int kX8K = 384, kX8KS = kX8K / 128, kX8BM = 256, kX8BN = 64, kX8Tile = kX8BN * kX8K, kX8R = 4;
+constexpr int kX8Pieces = kX8Tile / 1024 / 8;   // 3
+constexpr int kX8MaxN = 3072;
+
+template <int EPI, bool RS>
+__global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
+  static_assert(EPI == EPI_SWIGLU || EPI == EPI_STORE, "SWIGLU / STORE");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kX8R * kX8Tile + kX8MaxN * (kX8K / 32) + 4 * kX8MaxN];
+  uint8_t* sWs = lds + kX8R * kX8Tile;                         // W scales [N][12]
+  float* sb = reinterpret_cast<float*>(sWs + kX8MaxN * (kX8K / 32));
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, lg = lane >> 4, swz = (l15 >> 1) & 7;
+  const int nwt = p.N / kX8BN, ntm = (p.M + kX8BM - 1) / kX8BM, nch = (nwt + nc - 1) / nc;
+  const int items = ntm * nch;
+  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int q = (items + 7) >> 3, ibeg = xcd * q, iend = min(items, ibeg + q);
+  if (ibeg + jb >= iend) return;                                  // workgroup-uniform
+
+  for (int i = tid; i < p.N * (kX8K / 32); i += 512) sWs[i] = p.Ws[i];
+  for (int i = tid; i < p.N; i += 512) sb[i] = p.bias ? p.bias[i] : 0.f;
+  __syncthreads();                                                // no DMA in flight yet
+
+  auto dma = [&](int t) {
+    uint8_t* base = lds + (t % kX8R) * kX8Tile;
+    (void)base;
+#pragma unroll
+    for (int i = 0; i < kX8Pieces; ++i) {
+      const int pc = wid * kX8Pieces + i, lin = pc * 64 + lane, row = lin / 24, slot = lin % 24;
+      const uint8_t* src = p.W + (int64_t)(t * kX8BN + row) * kX8K + ((slot ^ ((row >> 1) & 7)) << 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + pc * 1024, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+
+  for (int item = ibeg + jb; item < iend; item += nxb) {
+    const int mt = item / nch, ch = item % nch;
+    const int t0 = ch * nc, t1 = min(nwt, t0 + nc), n = t1 - t0;
+    const int mbase = mt * kX8BM + wid * 32;
+
+    i32x8 xf[2][kX8KS];
+    int xs[2][kX8KS];
+    float inv[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int64_t row = min(mbase + 16 * mb + l15, p.M - 1);
+      const uint8_t* xr = p.A + row * p.lda;
+#pragma unroll
+      for (int ks = 0; ks < kX8KS; ++ks) {
+        const u32x4 a = *reinterpret_cast<const u32x4*>(xr + 128 * ks + 16 * lg);
+        const u32x4 b = *reinterpret_cast<const u32x4*>(xr + 128 * ks + 64 + 16 * lg);
+        xf[mb][ks] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+        xs[mb][ks] = p.As[row * p.ldas + 4 * ks + lg];
+      }
+      inv[mb] = RS ? p.rs_inv[row] : 1.0f;
+    }
+
+    f32x4 acc[2][2][4];   // [buffer][mb][nb]
+    auto epi_part = [&](int b, int t, int part) __attribute__((always_inline)) {
+      const int mb = part >> 1, hh = part & 1;
+      const int m = mbase + 16 * mb + l15;
+      const bool ok = m < p.M;
+      const int64_t mrow = min(m, p.M - 1);
+      if constexpr (EPI == EPI_SWIGLU) {
+        if (hh) return;                       // one MX block (32 h columns) per row and tile: both halves here
+        float v[8];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int ng = kX8BN * t + 16 * h2 + 4 * lg;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gg = fmaf(acc[b][mb][h2][r], inv[mb], sb[ng + r]);
+            const float uu = fmaf(acc[b][mb][2 + h2][r], inv[mb], sb[ng + 32 + r]);
+            v[4 * h2 + r] = gg * fsig(gg) * uu;
+          }
+        }
+        float am = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
+        am = fmaxf(am, __shfl_xor(am, 16, 64));
+        am = fmaxf(am, __shfl_xor(am, 32, 64));
+        const int e = mx_exp(am);
+        const u32x2 qv = quant8(v, exp2i(e));
+        const int col = 32 * t;                                   // first h column of the block
+        if (ok) {
+          *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 4 * lg) = qv[0];
+          *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 16 + 4 * lg) = qv[1];
+          if (lg == 0) p.C8s[mrow * p.ldc8s + t] = (uint8_t)e;
+        }
+      } else {
+#pragma unroll
+        for (int nb2 = 0; nb2 < 2; ++nb2) {
+          const int nb = 2 * hh + nb2, col = kX8BN * t + 16 * nb + 4 * lg;
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = fmaf(acc[b][mb][nb][r], inv[mb], sb[col + r]);
+          const __bf16 b0 = (__bf16)o[0], b1 = (__bf16)o[1], b2 = (__bf16)o[2], b3 = (__bf16)o[3];
+          const u32x2 w = {(uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16),
+                           (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16)};
+          if (ok) *reinterpret_cast<u32x2*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
+        }
+      }
+    };
+
+    // ring: tiles t0 .. t0 + R - 2 in flight before the loop; tile t + R - 1 issued at the end of tile t
+#pragma unroll
+    for (int s0 = 0; s0 < kX8R - 1; ++s0)
+      if (s0 < n) dma(t0 + s0);
+    auto tile = [&](auto Bc, int j) __attribute__((always_inline)) {
+      constexpr int b = decltype(Bc)::value;
+      const int t = t0 + j;
+      const int ahead = min(kX8R - 2, n - 1 - j);                 // younger tiles in flight
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kX8Pieces) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kX8Pieces) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds();
+      const uint8_t* base = lds + (t % kX8R) * kX8Tile;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) acc[b][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < kX8KS; ++ks) {
+        i32x8 wf[4];
+        int ws[4];
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+          const int row = 16 * nb + l15;
+          const uint8_t* r = base + row * kX8K;
+          const u32x4 a = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + lg) ^ swz));
+          const u32x4 c = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + 4 + lg) ^ swz));
+          wf[nb] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)c[0], (int)c[1], (int)c[2], (int)c[3]};
+          ws[nb] = sWs[(t * kX8BN + row) * (kX8K / 32) + 4 * ks + lg];
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc[b][mb][nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[nb], xf[mb][ks], acc[b][mb][nb], 0, 0, 0,
+                                                                              ws[nb], 0, xs[mb][ks]);
+        if (j > 0) {                                              // previous tile, under these MFMAs
+          if (ks == 0) epi_part(b ^ 1, t - 1, 0);
+          if (ks == 1) epi_part(b ^ 1, t - 1, 2);
+          if (ks == 2) { epi_part(b ^ 1, t - 1, 1); epi_part(b ^ 1, t - 1, 3); }
+        }
+        __builtin_amdgcn_sched_barrier(0);                        // keep each step's fragment reads in the step
+      }
+      if (j + kX8R - 1 < n) dma(t + kX8R - 1);                    // slot (t - 1) % R: every wave is past it
+    };
+    for (int j = 0; j < n; j += 2) {
+      tile(std::integral_constant<int, 0>{}, j);
+      if (j + 1 < n) tile(std::integral_constant<int, 1>{}, j + 1);
+    }
+    if ((n - 1) & 1) {
+#pragma unroll
+      for (int part = 0; part < 4; ++part) epi_part(1, t1 - 1, part);
+    } else {
+#pragma unroll
+      for (int part = 0; part < 4; ++part) epi_part(0, t1 - 1, part);
+    }
+    __syncthreads();
+  }
+}
+
+template <int EPI>
+hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
+  const int items = ((a.M + kX8BM - 1) / kX8BM) * ((a.N / kX8BN + nc - 1) / nc);
+  int grid = 256;
+  const int need = (items + 7) / 8 * 8;
+  if (grid > need) grid = need;
+  if (a.rs_inv) hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true>), dim3(grid), dim3(512), 0, st, a, nc);
+  else hipLaunchKernelGGL((gemm_xs8_kernel<EPI, false>), dim3(grid), dim3(512), 0, st, a, nc);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// X-stationary MXFP8 GEMM for K = 384 (gemm_xs8_kernel); nc = W tiles per work item (0: auto)
+hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st) {
+  if (a.K != kX8K || a.N % kX8BN || a.N > kX8MaxN || a.M <= 0 || a.lda % 16 || a.ldas != kX8K / 32 || a.R || a.C2)
+    return hipErrorInvalidValue;
+  if (epi == EPI_SWIGLU && (!a.C8 || !a.C8s || a.ldc % 16)) return hipErrorInvalidValue;
+  if (epi == EPI_STORE && (!a.c_bf16 || a.ldc % 8)) return hipErrorInvalidValue;
+  const int nwt = a.N / kX8BN, ntm = (a.M + kX8BM - 1) / kX8BM;
+  if (nc <= 0) {
+    double best = -1.0;
+    for (int c = nwt; c >= 1; --c) {
+      const int items = ntm * ((nwt + c - 1) / c);
+      const int rounds = (items + 255) / 256;
+      const double eff = (double)items / (256.0 * rounds) - (c < 4 ? 0.2 : 0.0) + 1e-3 * c;
+      if (eff > best) { best = eff; nc = c; }
+    }
+  }
+  switch (epi) {
+    case EPI_SWIGLU: return launch_xs8<EPI_SWIGLU>(a, nc, st);
+    case EPI_STORE: return launch_xs8<EPI_STORE>(a, nc, st);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t gemm_mx(const MxArgs& a0, int epi, hipStream_t st) {
   MxArgs a = a0;

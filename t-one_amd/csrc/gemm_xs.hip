@@ -1,0 +1,243 @@
+// X-stationary bf16 GEMM for the K = 384 encoder projections at large batch (FFN up + SwiGLU, pw1 + GLU,
+// q|k|v), computed in the transposed orientation D[n][m] = W[n][:] . X[m][:] like gemm_t.
+//
+// Why: with K = 384 a 256 x 256 output tile does only 2 * 256 * 256 * 384 FLOP per (256 + 256) x 384 x 2 bytes
+// staged through LDS (128 FLOP/B), and gemm_t's loop is bound by that LDS-DMA fill (~32 GB/s per CU) plus a
+// SwiGLU epilogue during which every wave of the CU idles the matrix pipe.  Here
+//   * one wave per SIMD (4 per workgroup, 512 registers each); each wave keeps ITS OWN 64 X rows x 384 K in
+//     registers for a whole work item (192 VGPRs of bf16 fragments, loaded once from L2 / HBM, with the
+//     folded-RMSNorm row sums taken from them), so only W
+//     streams through LDS: 64 W rows x 384 K (48 KiB) per tile for 2 x 64 x 256 x 384 FLOP = 262 FLOP/B,
+//     twice gemm_t's;
+//   * the W tiles go through a 3-deep LDS ring by global_load_lds_dwordx4, the tile two ahead issued at
+//     the end of each tile (after that tile's stores, so one counted vmcnt covers exactly the next tile);
+//     16-byte chunk c of W row r sits at LDS slot c ^ (r & 15) of its 768-byte row, which makes every
+//     ds_read_b128 of the 16x16x32 fragment map conflict-free;
+//   * the accumulators are small (4 m-blocks x 4 n-blocks x 4 per lane), so they are double-buffered: the
+//     epilogue of tile t - 1 (bias, SwiGLU / GLU, bf16 pack, stores) is interleaved with the MFMAs of tile
+//     t in the same wave instead of running with the matrix pipe idle.
+// Work item = (256 X rows, a run of nc W tiles); items are dealt so the items of one X row block share an
+// XCD (its X rows are fetched into one L2).  Epilogues (gemm.hip): SWIGLU / GLU on W rows interleaved in
+// 32-row blocks (one 64-row W tile = one g | u block pair -> 32 output columns), STORE (+bias, bf16 out).
+#include "common.h"
+#include "kernels.h"
+
+#include "gemm_common.h"
+
+#include <type_traits>
+
+namespace tone {
+namespace {
+
+constexpr int kXsK = 384;                 // K (d_model)
+constexpr int kXsKS = kXsK / 32;          // 16x16x32 K-steps
+constexpr int kXsWaves = 8;               // two waves per SIMD: 256 registers each
+constexpr int kXsMB = 2;                  // 16-row m-blocks per wave
+constexpr int kXsBM = kXsWaves * 16 * kXsMB;   // X rows per work item (256)
+constexpr int kXsBN = 64;                 // W rows per tile
+constexpr int kXsRowB = kXsK * 2;         // bytes per W row (768)
+constexpr int kXsTile = kXsBN * kXsRowB;  // 48 KiB
+constexpr int kXsR = 3;                   // W ring depth
+constexpr int kXsPieces = kXsTile / 1024 / kXsWaves;   // 1 KiB DMA pieces per wave per tile (12)
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t2 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pkb(float a, float b) {
+  const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+}
+
+template <int EPI, bool RS>
+__global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int nc) {
+  static_assert(EPI == EPI_SWIGLU || EPI == EPI_GLU || EPI == EPI_STORE, "SWIGLU / GLU / STORE");
+  constexpr bool PAIRED = (EPI != EPI_STORE);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kXsR * kXsTile + 4 * kBiasMax];
+  float* sbias = reinterpret_cast<float*>(lds + kXsR * kXsTile);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, lg = lane >> 4;
+  const int nwt = p.N / kXsBN, ntm = (p.M + kXsBM - 1) / kXsBM, nch = (nwt + nc - 1) / nc;
+  const int items = ntm * nch;
+  // items of one X row block are consecutive; deal contiguous item ranges to XCDs (blocks b, b + 8, ... share one)
+  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int q = (items + 7) >> 3, ibeg = xcd * q, iend = min(items, ibeg + q);
+  if (ibeg + jb >= iend) return;                                  // workgroup-uniform
+
+  for (int i = tid; i < p.N; i += kXsWaves * 64) sbias[i] = p.bias ? p.bias[i] : 0.f;
+  __syncthreads();                                                // no DMA in flight yet
+
+  const uint16_t* __restrict__ X = static_cast<const uint16_t*>(p.A);
+  const uint8_t* __restrict__ Wb = static_cast<const uint8_t*>(p.W);
+
+  // DMA of W tile t (global rows 64 t ..) into ring slot t % R: wave w moves pieces 6 w .. 6 w + 5; lane i of
+  // piece pc lands at linear 16-byte slot 64 pc + i of the tile = (row, slot) with 48 slots per row and
+  // fetches the chunk slot ^ (row & 15) of that row
+  auto dma = [&](int t) {
+    uint8_t* base = lds + (t % kXsR) * kXsTile;
+    (void)base;
+#pragma unroll
+    for (int i = 0; i < kXsPieces; ++i) {
+      const int pc = wid * kXsPieces + i, lin = pc * 64 + lane, row = lin / 48, slot = lin % 48;
+      const uint8_t* src = Wb + ((int64_t)(t * kXsBN + row) * kXsK) * 2 + ((slot ^ (row & 15)) << 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, base + pc * 1024, 16, 0, 0);
+#else
+      (void)src;
+#endif
+    }
+  };
+
+  for (int item = ibeg + jb; item < iend; item += nxb) {
+    const int mt = item / nch, ch = item % nch;
+    const int t0 = ch * nc, t1 = min(nwt, t0 + nc), n = t1 - t0;
+    const int mbase = mt * kXsBM + wid * 16 * kXsMB;              // this wave's 64 X rows
+
+    // this wave's X fragments: m-block mb, K-step ks -> lane holds row mbase + 16 mb + l15, k 32 ks + 8 lg ..
+    bf16x8_t xf[kXsMB][kXsKS];
+    float inv[kXsMB];
+#pragma unroll
+    for (int mb = 0; mb < kXsMB; ++mb) {
+      const int64_t row = min(mbase + 16 * mb + l15, p.M - 1);
+      const uint16_t* xr = X + row * p.lda + 8 * lg;
+      float ss = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < kXsKS; ++ks) {
+        xf[mb][ks] = *reinterpret_cast<const bf16x8_t*>(xr + 32 * ks);
+        if constexpr (RS) ss = sumsq8(xf[mb][ks], ss);
+      }
+      if constexpr (RS) {
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        inv[mb] = 1.0f / (sqrtf(ss) * p.inv_sqrt_k + kRmsEps);
+      } else {
+        inv[mb] = 1.0f;
+      }
+    }
+
+    f32x4_t2 acc[2][kXsMB][4];   // [buffer][mb][nb]
+    // epilogue of W tile t from accumulator buffer b (one eighth at a time: part = mb * 2 + half)
+    auto epi_part = [&](int b, int t, int part) __attribute__((always_inline)) {
+      const int mb = part >> 1, hh = part & 1;
+      const int m = mbase + 16 * mb + l15;
+      const bool ok = m < p.M;
+      const int64_t mrow = min(m, p.M - 1);
+      if constexpr (PAIRED) {
+        // g rows 16 nb + 4 lg + r (nb = hh), u rows 32 + 16 nb + 4 lg + r -> output column 32 t + 16 hh + 4 lg + r
+        const int ng = kXsBN * t + 16 * hh + 4 * lg;
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = fmaf(acc[b][mb][hh][r], inv[mb], sbias[ng + r]);
+          const float u = fmaf(acc[b][mb][2 + hh][r], inv[mb], sbias[ng + 32 + r]);
+          o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
+        }
+        const int col = 32 * t + 16 * hh + 4 * lg;
+        if (p.c_bf16) {
+          const u32x2_t w = {pkb(o[0], o[1]), pkb(o[2], o[3])};
+          if (ok) *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
+        } else {
+          const f32x4_t2 w = {o[0], o[1], o[2], o[3]};
+          if (ok) *reinterpret_cast<f32x4_t2*>(static_cast<float*>(p.C) + mrow * p.ldc + col) = w;
+        }
+      } else {
+#pragma unroll
+        for (int nb2 = 0; nb2 < 2; ++nb2) {
+          const int nb = 2 * hh + nb2, col = kXsBN * t + 16 * nb + 4 * lg;
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = fmaf(acc[b][mb][nb][r], inv[mb], sbias[col + r]);
+          const u32x2_t w = {pkb(o[0], o[1]), pkb(o[2], o[3])};
+          if (ok) *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
+        }
+      }
+    };
+
+    // ring prologue
+    dma(t0);
+    if (n > 1) dma(t0 + 1);
+    // one W tile; the accumulator buffer is a compile-time index (B), so the tile loop is unrolled by two
+    auto tile = [&](auto Bc, int j) __attribute__((always_inline)) {
+      constexpr int b = decltype(Bc)::value;
+      const int t = t0 + j;
+      if (j + 1 < n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kXsPieces) : "memory");   // tile t landed
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds();                                              // ... for every wave; slot (t - 1) % R free
+      const uint8_t* base = lds + (t % kXsR) * kXsTile;
+#pragma unroll
+      for (int mb = 0; mb < kXsMB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) acc[b][mb][nb] = f32x4_t2{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < kXsKS; ++ks) {
+        bf16x8_t wf[4];
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+          const int row = 16 * nb + l15, c = 4 * ks + lg;
+          wf[nb] = *reinterpret_cast<const bf16x8_t*>(base + row * kXsRowB + ((c ^ l15) << 4));
+        }
+#pragma unroll
+        for (int mb = 0; mb < kXsMB; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc[b][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nb], xf[mb][ks], acc[b][mb][nb], 0, 0, 0);
+        // previous tile's epilogue, one part every other K-step, under these MFMAs
+        if (j > 0 && ks % 2 == 1 && ks / 2 < 2 * kXsMB) epi_part(b ^ 1, t - 1, ks / 2);
+        __builtin_amdgcn_sched_barrier(0);                        // keep each step's fragment reads in the step
+      }
+      if (j + 2 < n) dma(t + 2);                                   // into slot (t - 1) % R, read by nobody now
+    };
+    for (int j = 0; j < n; j += 2) {
+      tile(std::integral_constant<int, 0>{}, j);
+      if (j + 1 < n) tile(std::integral_constant<int, 1>{}, j + 1);
+    }
+    if ((n - 1) & 1) {
+#pragma unroll
+      for (int part = 0; part < 2 * kXsMB; ++part) epi_part(1, t1 - 1, part);
+    } else {
+#pragma unroll
+      for (int part = 0; part < 2 * kXsMB; ++part) epi_part(0, t1 - 1, part);
+    }
+    __syncthreads();                                              // the ring is reused by the next item
+  }
+}
+
+template <int EPI>
+hipError_t launch_xs(const GemmArgs& a, int nc, hipStream_t st) {
+  const int items = ((a.M + kXsBM - 1) / kXsBM) * ((a.N / kXsBN + nc - 1) / nc);
+  int grid = 256;
+  const int need = (items + 7) / 8 * 8;
+  if (grid > need) grid = need;
+  if (a.rowscale) hipLaunchKernelGGL((gemm_xs_kernel<EPI, true>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
+  else hipLaunchKernelGGL((gemm_xs_kernel<EPI, false>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// nc = W tiles per work item (0: chosen so the items fill the 256 CUs in whole rounds)
+hipError_t gemm_xs(const GemmArgs& a, int epi, int nc, hipStream_t st) {
+  if (!a.a_bf16 || a.K != kXsK || a.N % kXsBN || a.N > kBiasMax || a.M <= 0 || a.rpg || a.lda % 8 || a.ldc % 8 ||
+      a.k_split || a.C2)
+    return hipErrorInvalidValue;
+  if (epi == EPI_STORE && !a.c_bf16) return hipErrorInvalidValue;
+  const int nwt = a.N / kXsBN, ntm = (a.M + kXsBM - 1) / kXsBM;
+  if (nc <= 0) {   // the run length with the best round efficiency (items / (256 * rounds)), >= 4 tiles preferred
+    double best = -1.0;
+    for (int c = nwt; c >= 1; --c) {
+      const int items = ntm * ((nwt + c - 1) / c);
+      const int rounds = (items + 255) / 256;
+      const double eff = (double)items / (256.0 * rounds) - (c < 4 ? 0.2 : 0.0) + 1e-3 * c;
+      if (eff > best) { best = eff; nc = c; }
+    }
+  }
+  switch (epi) {
+    case EPI_SWIGLU: return launch_xs<EPI_SWIGLU>(a, nc, st);
+    case EPI_GLU: return launch_xs<EPI_GLU>(a, nc, st);
+    case EPI_STORE: return launch_xs<EPI_STORE>(a, nc, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tone

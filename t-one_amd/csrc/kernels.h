@@ -91,6 +91,8 @@ struct MxArgs {
   int prio;               // static priority for waves 4-7 (set by gemm_mx(), TONE_PRIO_MX)
 };
 hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st);
+// X-stationary MXFP8 GEMM for K = 384 (gemm_mx.hip gemm_xs8_kernel): SWIGLU (-> MXFP8 h) / STORE (bf16 out)
+hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st);
 // bf16 [M][K] (ldx elements) -> e4m3 [M][K] + E8M0 [M][K/32]; inv (optional): 1/(||row||/sqrt(K) + 1e-8)
 hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t* Q, uint8_t* S, float* inv,
                            hipStream_t st);
@@ -98,6 +100,9 @@ hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // persistent transposed-orientation bf16 GEMM (gemm_t.hip); variant = tile shape, see there
 hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
+// X-stationary bf16 GEMM for K = 384 (gemm_xs.hip): X rows in registers, W tiles streamed through an LDS ring,
+// epilogue overlapped with the next tile's MFMAs; SWIGLU / GLU / STORE (bf16 out); nc = W tiles per work item (0: auto)
+hipError_t gemm_xs(const GemmArgs& a, int epi, int nc, hipStream_t st);
 // exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3

@@ -126,7 +126,10 @@ __global__ void ref_mx_kernel(const float* A, const float* W, const float* bias,
 }
 
 static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, const float* R, float* ref, float* err,
-                   int M, int N, int K, int epi, int rowscale, int iters) {
+                   int M, int N, int K, int epi, int rowscale, int iters, int xs = 0) {
+  // xs: 98 = the X-stationary kernel (gemm_xs8, SWIGLU only; XSNC = W tiles per item, 0 auto)
+  const int xsnc = getenv("XSNC") ? atoi(getenv("XSNC")) : 0;
+  auto mx = [&](const MxArgs& a) { return xs ? gemm_xs8(a, epi, xsnc, 0) : gemm_mx(a, epi, 0); };
   const int nout = epi >= 2 ? N / 2 : N;
   uint8_t *A8, *As, *W8, *Ws, *C8, *C8s;
   float *inv, *Af, *Wf, *C, *Cf;
@@ -147,8 +150,8 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   a.C8 = C8; a.C8s = C8s; a.ldc8s = nout / 32; a.M = M; a.N = N; a.K = K;
   a.dbg = getenv("MXDBG") ? atoi(getenv("MXDBG")) : 0;   // gemm_mx.hip DBG bits (SWIGLU only)
   if (epi >= 2) a.ldc = nout;   // bytes of C8 rows
-  hipError_t rc = gemm_mx(a, epi, 0);
-  if (rc != hipSuccess) { printf("{\"variant\": 99, \"error\": \"%s\"}\n", hipGetErrorString(rc)); return; }
+  hipError_t rc = mx(a);
+  if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", xs ? 98 : 99, hipGetErrorString(rc)); return; }
   CK(hipDeviceSynchronize());
   const float* chk = C;
   if (epi >= 2) {
@@ -161,9 +164,9 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) CK(gemm_mx(a, epi, 0));
+  for (int i = 0; i < 3; ++i) CK(mx(a));
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK(gemm_mx(a, epi, 0));
+  for (int i = 0; i < iters; ++i) CK(mx(a));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -175,8 +178,8 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   CK(hipEventSynchronize(e1));
   float qms;
   CK(hipEventElapsedTime(&qms, e0, e1));
-  printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": 99, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"quant_us\": %.2f}\n",
-         M, K, N, epi, us, 2.0 * M * N * (double)K / us * 1e-6, herr, qms * 1e3 / iters);
+  printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"quant_us\": %.2f}\n",
+         M, K, N, epi, xs ? 98 : 99, us, 2.0 * M * N * (double)K / us * 1e-6, herr, qms * 1e3 / iters);
   fflush(stdout);
 }
 
@@ -263,8 +266,8 @@ int main(int argc, char** argv) {
   char* list = strdup(argv[5]);
   for (char* tok = strtok(list, ","); tok; tok = strtok(nullptr, ",")) {
     const int vv = atoi(tok);
-    if (vv == 99) {   // MXFP8 path: quant_mx + gemm_mx vs an fp64 reference on the dequantized operands
-      run_mx(A, W, bias, R, ref, err, M, N, K, epi, rowscale, iters);
+    if (vv == 99 || vv == 98) {   // MXFP8 path: quant_mx + gemm_mx (99) / gemm_xs8 (98) vs an fp64 reference
+      run_mx(A, W, bias, R, ref, err, M, N, K, epi, rowscale, iters, vv == 98);
       continue;
     }
     // v % 100 = variant (20..23: gemm_t tiles); (v / 100) bits: 1 N-partitioned XCD order,
@@ -285,7 +288,8 @@ int main(int argc, char** argv) {
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
-      return v < 0 ? gemm(a, epi, !f32, 0)
+      return vv <= -10 ? gemm_xs(a, epi, -10 - vv, 0)      // -10: gemm_xs auto run length, -10 - c: c W tiles per item
+             : v < 0 ? gemm(a, epi, !f32, 0)
              : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
              : (v >= 50 && nsplit > 1) ? gemm_x3_splitk(a, epi, v - 50, nsplit, 0)
