@@ -98,6 +98,38 @@ __device__ __forceinline__ float exp2i(int ebiased) {
   return __uint_as_float((uint32_t)(254 - ebiased) << 23);
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform n known only at run time (a scalar branch to the immediate form)
+__device__ __forceinline__ void vmcnt_dyn(int n) {
+  switch (n) {
+#define TONE_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    TONE_VMC(1) TONE_VMC(2) TONE_VMC(3) TONE_VMC(4) TONE_VMC(5) TONE_VMC(6) TONE_VMC(7) TONE_VMC(8) TONE_VMC(9)
+    TONE_VMC(10) TONE_VMC(11) TONE_VMC(12) TONE_VMC(13) TONE_VMC(14) TONE_VMC(15) TONE_VMC(16) TONE_VMC(17)
+    TONE_VMC(18) TONE_VMC(19) TONE_VMC(20) TONE_VMC(21) TONE_VMC(22) TONE_VMC(23) TONE_VMC(24) TONE_VMC(25)
+    TONE_VMC(26) TONE_VMC(27) TONE_VMC(28) TONE_VMC(29) TONE_VMC(30) TONE_VMC(31) TONE_VMC(32)
+#undef TONE_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// Counted wait for an LDS-DMA ring of depth R over n tiles where tile t + R - 1's P pieces are issued at the START
+// of iteration t (tiles 0 .. R - 2 before the loop) and iteration i >= 1 then issues S stores (the epilogue of tile
+// i - 1): the number of this wave's vector-memory ops issued after tile j's DMA, i.e. the vmcnt that guarantees
+// tile j landed.  (Ops the compiler adds only make the wait stricter.)
+__device__ __forceinline__ int ring_younger(int j, int n, int R, int P, int S) {
+  int c = 0;
+  int i0;
+  if (j <= R - 2) {
+    for (int t = j + 1; t <= R - 2; ++t) c += (t < n) ? P : 0;   // later prologue tiles
+    i0 = 0;
+  } else {
+    i0 = j - R + 1;                                            // the iteration that issued tile j ...
+    c += (i0 >= 1) ? S : 0;                                    // ... and its stores after it
+    ++i0;
+  }
+  for (int i = i0; i < j; ++i) c += ((i + R - 1 < n) ? P : 0) + ((i >= 1) ? S : 0);
+  return c;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -410,6 +410,7 @@ constexpr int kX8MaxN = 3072;
 template <int EPI, bool RS>
 __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_STORE, "SWIGLU / STORE");
+  constexpr int kStores8 = EPI == EPI_SWIGLU ? 2 * 3 : 4 * 2;      // vector stores per tile epilogue (per lane)
   __shared__ __attribute__((aligned(16))) uint8_t lds[kX8R * kX8Tile + kX8MaxN * (kX8K / 32) + 4 * kX8MaxN];
   uint8_t* sWs = lds + kX8R * kX8Tile;                         // W scales [N][12]
   float* sb = reinterpret_cast<float*>(sWs + kX8MaxN * (kX8K / 32));
@@ -466,9 +467,8 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
     f32x4 acc[2][2][4];   // [buffer][mb][nb]
     auto epi_part = [&](int b, int t, int part) __attribute__((always_inline)) {
       const int mb = part >> 1, hh = part & 1;
-      const int m = mbase + 16 * mb + l15;
-      const bool ok = m < p.M;
-      const int64_t mrow = min(m, p.M - 1);
+      // every lane stores (fixed count per tile for the counted vmcnt): a row past M rewrites row M - 1's values
+      const int64_t mrow = min(mbase + 16 * mb + l15, p.M - 1);
       if constexpr (EPI == EPI_SWIGLU) {
         if (hh) return;                       // one MX block (32 h columns) per row and tile: both halves here
         float v[8];
@@ -490,11 +490,9 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
         const int e = mx_exp(am);
         const u32x2 qv = quant8(v, exp2i(e));
         const int col = 32 * t;                                   // first h column of the block
-        if (ok) {
-          *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 4 * lg) = qv[0];
-          *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 16 + 4 * lg) = qv[1];
-          if (lg == 0) p.C8s[mrow * p.ldc8s + t] = (uint8_t)e;
-        }
+        *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 4 * lg) = qv[0];
+        *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 16 + 4 * lg) = qv[1];
+        p.C8s[mrow * p.ldc8s + t] = (uint8_t)e;                   // the 4 lanes of the block write the same byte
       } else {
 #pragma unroll
         for (int nb2 = 0; nb2 < 2; ++nb2) {
@@ -505,32 +503,27 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           const __bf16 b0 = (__bf16)o[0], b1 = (__bf16)o[1], b2 = (__bf16)o[2], b3 = (__bf16)o[3];
           const u32x2 w = {(uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16),
                            (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16)};
-          if (ok) *reinterpret_cast<u32x2*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
+          *reinterpret_cast<u32x2*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
         }
       }
     };
 
-    // ring: tiles t0 .. t0 + R - 2 in flight before the loop; tile t + R - 1 issued at the end of tile t
+    // ring: tiles t0 .. t0 + R - 2 in flight before the loop; tile t + R - 1 issued at the start of tile t
 #pragma unroll
     for (int s0 = 0; s0 < kX8R - 1; ++s0)
       if (s0 < n) dma(t0 + s0);
     auto tile = [&](auto Bc, int j) __attribute__((always_inline)) {
       constexpr int b = decltype(Bc)::value;
       const int t = t0 + j;
-      const int ahead = min(kX8R - 2, n - 1 - j);                 // younger tiles in flight
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kX8Pieces) : "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kX8Pieces) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      barrier_lds();
+      vmcnt_dyn(ring_younger(j, n, kX8R, kX8Pieces, kStores8));   // tile t landed
+      barrier_lds();                                              // ... for every wave; slot (t - 1) % R free
+      if (j + kX8R - 1 < n) dma(t + kX8R - 1);
       const uint8_t* base = lds + (t % kX8R) * kX8Tile;
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) acc[b][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < kX8KS; ++ks) {
-        i32x8 wf[4];
-        int ws[4];
+      auto rdw = [&](int ks, i32x8 (&wf)[4], int (&ws)[4]) __attribute__((always_inline)) {
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) {
           const int row = 16 * nb + l15;
@@ -539,6 +532,18 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           const u32x4 c = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + 4 + lg) ^ swz));
           wf[nb] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)c[0], (int)c[1], (int)c[2], (int)c[3]};
           ws[nb] = sWs[(t * kX8BN + row) * (kX8K / 32) + 4 * ks + lg];
+        }
+      };
+      i32x8 wa[4], wb[4];
+      int sa[4], sbw[4];
+      rdw(0, wa, sa);
+#pragma unroll
+      for (int ks = 0; ks < kX8KS; ++ks) {
+        i32x8(&wf)[4] = (ks & 1) ? wb : wa;
+        int(&ws)[4] = (ks & 1) ? sbw : sa;
+        if (ks + 1 < kX8KS) {
+          if (ks & 1) rdw(ks + 1, wa, sa);
+          else rdw(ks + 1, wb, sbw);
         }
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
@@ -551,9 +556,8 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           if (ks == 1) epi_part(b ^ 1, t - 1, 2);
           if (ks == 2) { epi_part(b ^ 1, t - 1, 1); epi_part(b ^ 1, t - 1, 3); }
         }
-        __builtin_amdgcn_sched_barrier(0);                        // keep each step's fragment reads in the step
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (j + kX8R - 1 < n) dma(t + kX8R - 1);                    // slot (t - 1) % R: every wave is past it
     };
     for (int j = 0; j < n; j += 2) {
       tile(std::integral_constant<int, 0>{}, j);
@@ -585,7 +589,7 @@ hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
 
 // X-stationary MXFP8 GEMM for K = 384 (gemm_xs8_kernel); nc = W tiles per work item (0: auto)
 hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st) {
-  if (a.K != kX8K || a.N % kX8BN || a.N > kX8MaxN || a.M <= 0 || a.lda % 16 || a.ldas != kX8K / 32 || a.R || a.C2)
+  if (a.K != kX8K || a.N % kX8BN || a.N > kX8MaxN || a.M <= 0 || a.lda % 16 || a.ldas != kX8K / 32 || a.C2)
     return hipErrorInvalidValue;
   if (epi == EPI_SWIGLU && (!a.C8 || !a.C8s || a.ldc % 16)) return hipErrorInvalidValue;
   if (epi == EPI_STORE && (!a.c_bf16 || a.ldc % 8)) return hipErrorInvalidValue;

@@ -9,8 +9,10 @@
 //     folded-RMSNorm row sums taken from them), so only W
 //     streams through LDS: 64 W rows x 384 K (48 KiB) per tile for 2 x 64 x 256 x 384 FLOP = 262 FLOP/B,
 //     twice gemm_t's;
-//   * the W tiles go through a 3-deep LDS ring by global_load_lds_dwordx4, the tile two ahead issued at
-//     the end of each tile (after that tile's stores, so one counted vmcnt covers exactly the next tile);
+//   * the W tiles go through a 3-deep LDS ring by global_load_lds_dwordx4, tile t + 2 issued as soon as tile t
+//     starts (its slot held tile t - 1, whose reads every wave finished before the barrier), so a tile has two
+//     tiles of MFMAs to land; every lane issues a fixed number of stores per tile, which keeps the counted
+//     vmcnt exact;
 //     16-byte chunk c of W row r sits at LDS slot c ^ (r & 15) of its 768-byte row, which makes every
 //     ds_read_b128 of the 16x16x32 fragment map conflict-free;
 //   * the accumulators are small (4 m-blocks x 4 n-blocks x 4 per lane), so they are double-buffered: the
@@ -53,6 +55,7 @@ template <int EPI, bool RS>
 __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_GLU || EPI == EPI_STORE, "SWIGLU / GLU / STORE");
   constexpr bool PAIRED = (EPI != EPI_STORE);
+  constexpr int kStores = 2 * kXsMB * (PAIRED ? 1 : 2);           // vector stores per tile epilogue (per lane)
   __shared__ __attribute__((aligned(16))) uint8_t lds[kXsR * kXsTile + 4 * kBiasMax];
   float* sbias = reinterpret_cast<float*>(lds + kXsR * kXsTile);
 
@@ -120,9 +123,9 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
     // epilogue of W tile t from accumulator buffer b (one eighth at a time: part = mb * 2 + half)
     auto epi_part = [&](int b, int t, int part) __attribute__((always_inline)) {
       const int mb = part >> 1, hh = part & 1;
-      const int m = mbase + 16 * mb + l15;
-      const bool ok = m < p.M;
-      const int64_t mrow = min(m, p.M - 1);
+      // every lane stores (the counted vmcnt below relies on a fixed number of stores per tile): a row past M
+      // holds row M - 1's values (its X fragments were clamped to that row), so it rewrites them unchanged
+      const int64_t mrow = min(mbase + 16 * mb + l15, p.M - 1);
       if constexpr (PAIRED) {
         // g rows 16 nb + 4 lg + r (nb = hh), u rows 32 + 16 nb + 4 lg + r -> output column 32 t + 16 hh + 4 lg + r
         const int ng = kXsBN * t + 16 * hh + 4 * lg;
@@ -136,10 +139,10 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
         const int col = 32 * t + 16 * hh + 4 * lg;
         if (p.c_bf16) {
           const u32x2_t w = {pkb(o[0], o[1]), pkb(o[2], o[3])};
-          if (ok) *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
+          *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
         } else {
           const f32x4_t2 w = {o[0], o[1], o[2], o[3]};
-          if (ok) *reinterpret_cast<f32x4_t2*>(static_cast<float*>(p.C) + mrow * p.ldc + col) = w;
+          *reinterpret_cast<f32x4_t2*>(static_cast<float*>(p.C) + mrow * p.ldc + col) = w;
         }
       } else {
 #pragma unroll
@@ -149,44 +152,53 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = fmaf(acc[b][mb][nb][r], inv[mb], sbias[col + r]);
           const u32x2_t w = {pkb(o[0], o[1]), pkb(o[2], o[3])};
-          if (ok) *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
+          *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
         }
       }
     };
 
-    // ring prologue
+    // ring prologue (dbg bits, microbenchmarks only: 1 no epilogue in the loop, 2 no MFMA, 4 DMA in the prologue only)
     dma(t0);
     if (n > 1) dma(t0 + 1);
     // one W tile; the accumulator buffer is a compile-time index (B), so the tile loop is unrolled by two
     auto tile = [&](auto Bc, int j) __attribute__((always_inline)) {
       constexpr int b = decltype(Bc)::value;
       const int t = t0 + j;
-      if (j + 1 < n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kXsPieces) : "memory");   // tile t landed
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // tile t landed (ring_younger: the ops issued after its DMA -- later DMAs and the fixed-count stores)
+      vmcnt_dyn(ring_younger(j, n, kXsR, kXsPieces, kStores));
       barrier_lds();                                              // ... for every wave; slot (t - 1) % R free
+      if (j + 2 < n && !(p.dbg & 4)) dma(t + 2);                   // two tiles of lead
       const uint8_t* base = lds + (t % kXsR) * kXsTile;
 #pragma unroll
       for (int mb = 0; mb < kXsMB; ++mb)
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) acc[b][mb][nb] = f32x4_t2{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < kXsKS; ++ks) {
-        bf16x8_t wf[4];
+      // W fragments one K-step ahead of the MFMAs that use them (two register sets), so the LDS latency of step
+      // ks + 1 hides under step ks's MFMAs
+      auto rdw = [&](int ks, bf16x8_t (&wf)[4]) __attribute__((always_inline)) {
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) {
           const int row = 16 * nb + l15, c = 4 * ks + lg;
           wf[nb] = *reinterpret_cast<const bf16x8_t*>(base + row * kXsRowB + ((c ^ l15) << 4));
         }
+      };
+      bf16x8_t wa[4], wb[4];
+      rdw(0, wa);
+#pragma unroll
+      for (int ks = 0; ks < kXsKS; ++ks) {
+        bf16x8_t(&cur)[4] = (ks & 1) ? wb : wa;
+        bf16x8_t(&nxt)[4] = (ks & 1) ? wa : wb;
+        if (ks + 1 < kXsKS) rdw(ks + 1, nxt);
 #pragma unroll
         for (int mb = 0; mb < kXsMB; ++mb)
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb)
-            acc[b][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nb], xf[mb][ks], acc[b][mb][nb], 0, 0, 0);
+            acc[b][mb][nb] = (p.dbg & 2) ? acc[b][mb][nb] + (float)cur[nb][0] * (float)xf[mb][ks][1]
+                                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[nb], xf[mb][ks], acc[b][mb][nb], 0, 0, 0);
         // previous tile's epilogue, one part every other K-step, under these MFMAs
-        if (j > 0 && ks % 2 == 1 && ks / 2 < 2 * kXsMB) epi_part(b ^ 1, t - 1, ks / 2);
-        __builtin_amdgcn_sched_barrier(0);                        // keep each step's fragment reads in the step
+        if (j > 0 && ks % 2 == 1 && ks / 2 < 2 * kXsMB && !(p.dbg & 1)) epi_part(b ^ 1, t - 1, ks / 2);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (j + 2 < n) dma(t + 2);                                   // into slot (t - 1) % R, read by nobody now
     };
     for (int j = 0; j < n; j += 2) {
       tile(std::integral_constant<int, 0>{}, j);

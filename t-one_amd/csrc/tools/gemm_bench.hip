@@ -277,6 +277,7 @@ int main(int argc, char** argv) {
     a.order_n = fl & 1;
     a.nt_store = (fl >> 1) & 1;
     a.dbg = (fl >> 2) & 255;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA; gemm_r3: see gemm_t.hip
+    if (vv <= -10 && getenv("XSDBG")) a.dbg = atoi(getenv("XSDBG"));   // gemm_xs ablations
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
     const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 50) || (v >= 50 && v < 90);

@@ -584,3 +584,22 @@ def test_hip_vs_exported_fp16_graph(sess):
     d = np.concatenate([x.ravel() for x in ds])
     print(f"HIP fp32 vs exported fp16 graph: max {d.max():.3g}, mean {d.mean():.3g}")
     assert d.max() < 2.5e-2 and d.mean() < 5e-3, (d.max(), d.mean())
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp8"])
+def test_nan_propagates(weights, prec):
+    """A NaN inside the step reaches the logprobs in every precision: one NaN in an FFN up-projection
+    bias makes one column of the SwiGLU output NaN, which fp8 mode quantizes to MXFP8 inside the GEMM epilogue --
+    that quantization must encode it as the e4m3 NaN, not clamp it to a finite -448."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    w = dict(weights)
+    b = w["encoder.layers.3.feed_forward1.linear1.bias"].copy()
+    b[5] = np.nan
+    w["encoder.layers.3.feed_forward1.linear1.bias"] = b
+    s = ToneSession(w, precision=prec, max_batch=4)
+    try:
+        lp, _ = gpu_step(s, synthetic_pcm(np.random.default_rng(2), 4, 0.0), np.zeros((4, C.STATE_SIZE), np.float16))
+    finally:
+        s.close()
+    assert np.isnan(lp).all(), f"{prec}: {np.isnan(lp).mean():.3f} of the logprobs are NaN"
