@@ -20,6 +20,9 @@ if [ "${SWEEP:-1}" = 1 ]; then
   sw $B 40960 1536 384 1 14,28,29 1 20
   echo "sweep done"
 fi
+if [ "${BENCH:-0}" = 1 ]; then
+  run r03_bench 600 python -u bench.py --cpu-baseline-s 2
+fi
 if [ "${SUITE:-1}" = 1 ]; then
   run r03_smoke 300 python __graft_entry__.py smoke
   run r03_gpu_all 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread

@@ -282,7 +282,8 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
 
 // ---------------------------------------------------------------------------------------------
 // ConformerConvolution depthwise part (conformer_blocks.py:427-433, submodules.py:364-402):
-//   x = [conv state (30) ; g (T)] per channel; next state = x[-30:]
+//   x = [conv state (30) ; g (T)] per channel; next state = x[-30:]; g (the GLU output) and out are bf16 in the
+//   bf16 / fp8 modes (OBF), fp32 in fp32 mode
 //   out[t] = SiLU(BN(bias + sum_k w[k] x[t+k]))  with BN folded into (w, b) on the host.
 // A workgroup of CPW threads (a thread per channel) handles NS streams x CPW channels, the channel's 31
 // taps (stored tap-major) in registers: 192 x 1 stream at large batch, 128 x 1 at small batch (B = 256:
@@ -292,7 +293,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
 // the enclosing 16-byte-aligned window and the two partial end vectors are written element-wise.
 constexpr int kDwSec = kD * kConvS;          // 11520 halves per (stream, layer)
 template <int T, bool OBF, int CPW, int NS>
-__global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g, StateRef s, int layer,
+__global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g, StateRef s, int layer,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      void* __restrict__ out, int B) {
   constexpr int kSec = CPW * kConvS;           // halves of this workgroup's slice
@@ -321,7 +322,7 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
   for (int si = 0; si < NS; ++si) {
     const int b = min(blockIdx.x * NS + si, B - 1);
 #pragma unroll
-    for (int t = 0; t < T; ++t) gx[si][t] = g[((int64_t)b * T + t) * kD + ch];
+    for (int t = 0; t < T; ++t) gx[si][t] = load_act<OBF>(g, ((int64_t)b * T + t) * kD + ch);
   }
   __syncthreads();
 #pragma unroll
@@ -371,7 +372,7 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const float* __restrict__ g
 }
 
 template <int T, bool OBF>
-static hipError_t launch_dwconv_t(const float* g, StateRef s, int layer, const float* w, const float* b, void* out,
+static hipError_t launch_dwconv_t(const void* g, StateRef s, int layer, const float* w, const float* b, void* out,
                                   int B, hipStream_t st) {
   const int forced = knobs().dwconv_variant;   // TONE_DWCONV_VARIANT (sweeps only): 0 = 384x2, 1 = 128x1, 2 = 384x1, 3 = 192x1
   const int v = forced >= 0 ? forced : (B >= 1024 ? 3 : 1);   // profiles/r01_dwconv_sweep.txt
@@ -386,7 +387,7 @@ static hipError_t launch_dwconv_t(const float* g, StateRef s, int layer, const f
   return hipGetLastError();
 }
 
-hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
+hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
                          int T, int B, hipStream_t st) {
   if (T == kT) return obf ? launch_dwconv_t<kT, true>(g, s, layer, w, b, out, B, st)
                           : launch_dwconv_t<kT, false>(g, s, layer, w, b, out, B, st);

@@ -594,15 +594,7 @@ hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st) {
   if (epi == EPI_SWIGLU && (!a.C8 || !a.C8s || a.ldc % 16)) return hipErrorInvalidValue;
   if (epi == EPI_STORE && (!a.c_bf16 || a.ldc % 8)) return hipErrorInvalidValue;
   const int nwt = a.N / kX8BN, ntm = (a.M + kX8BM - 1) / kX8BM;
-  if (nc <= 0) {
-    double best = -1.0;
-    for (int c = nwt; c >= 1; --c) {
-      const int items = ntm * ((nwt + c - 1) / c);
-      const int rounds = (items + 255) / 256;
-      const double eff = (double)items / (256.0 * rounds) - (c < 4 ? 0.2 : 0.0) + 1e-3 * c;
-      if (eff > best) { best = eff; nc = c; }
-    }
-  }
+  if (nc <= 0) nc = xs_run_length(ntm, nwt);
   switch (epi) {
     case EPI_SWIGLU: return launch_xs8<EPI_SWIGLU>(a, nc, st);
     case EPI_STORE: return launch_xs8<EPI_STORE>(a, nc, st);

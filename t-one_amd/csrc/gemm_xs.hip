@@ -51,7 +51,9 @@ __device__ __forceinline__ uint32_t pkb(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
 }
 
-template <int EPI, bool RS>
+// DBG (XS_ABLATE microbenchmark builds only): 1 no epilogue in the loop, 2 no MFMA, 4 W DMA in the prologue only,
+// 8 explicit K-step schedule, 16 no W reads from LDS, 32 no X loads
+template <int EPI, bool RS, bool OBF, int DBG = 0>
 __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_GLU || EPI == EPI_STORE, "SWIGLU / GLU / STORE");
   constexpr bool PAIRED = (EPI != EPI_STORE);
@@ -107,7 +109,8 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
       float ss = 0.f;
 #pragma unroll
       for (int ks = 0; ks < kXsKS; ++ks) {
-        xf[mb][ks] = *reinterpret_cast<const bf16x8_t*>(xr + 32 * ks);
+        if constexpr (DBG & 32) xf[mb][ks] = bf16x8_t{} + (__bf16)(float)(lane + ks + item);
+        else xf[mb][ks] = *reinterpret_cast<const bf16x8_t*>(xr + 32 * ks);
         if constexpr (RS) ss = sumsq8(xf[mb][ks], ss);
       }
       if constexpr (RS) {
@@ -137,7 +140,7 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
           o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
         }
         const int col = 32 * t + 16 * hh + 4 * lg;
-        if (p.c_bf16) {
+        if constexpr (OBF) {
           const u32x2_t w = {pkb(o[0], o[1]), pkb(o[2], o[3])};
           *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
         } else {
@@ -157,17 +160,19 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
       }
     };
 
-    // ring prologue (dbg bits, microbenchmarks only: 1 no epilogue in the loop, 2 no MFMA, 4 DMA in the prologue only)
+    // ring prologue
     dma(t0);
     if (n > 1) dma(t0 + 1);
     // one W tile; the accumulator buffer is a compile-time index (B), so the tile loop is unrolled by two
-    auto tile = [&](auto Bc, int j) __attribute__((always_inline)) {
+    // (the first tile of an item, F = true, has no previous epilogue: peeled so no branch splits the K-steps)
+    auto tile = [&](auto Bc, auto Fc, int j) __attribute__((always_inline)) {
       constexpr int b = decltype(Bc)::value;
+      constexpr bool first = decltype(Fc)::value;
       const int t = t0 + j;
       // tile t landed (ring_younger: the ops issued after its DMA -- later DMAs and the fixed-count stores)
       vmcnt_dyn(ring_younger(j, n, kXsR, kXsPieces, kStores));
       barrier_lds();                                              // ... for every wave; slot (t - 1) % R free
-      if (j + 2 < n && !(p.dbg & 4)) dma(t + 2);                   // two tiles of lead
+      if (j + 2 < n && !(DBG & 4)) dma(t + 2);                   // two tiles of lead
       const uint8_t* base = lds + (t % kXsR) * kXsTile;
 #pragma unroll
       for (int mb = 0; mb < kXsMB; ++mb)
@@ -183,26 +188,42 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
         }
       };
       bf16x8_t wa[4], wb[4];
-      rdw(0, wa);
+      if constexpr (DBG & 16) {   // no LDS reads: fragments from X (the operands still feed the keep-alive)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) wa[nb] = wb[nb] = xf[0][nb];
+      } else {
+        rdw(0, wa);
+      }
 #pragma unroll
       for (int ks = 0; ks < kXsKS; ++ks) {
         bf16x8_t(&cur)[4] = (ks & 1) ? wb : wa;
         bf16x8_t(&nxt)[4] = (ks & 1) ? wa : wb;
-        if (ks + 1 < kXsKS) rdw(ks + 1, nxt);
+        if (ks + 1 < kXsKS && !(DBG & 16)) rdw(ks + 1, nxt);
 #pragma unroll
         for (int mb = 0; mb < kXsMB; ++mb)
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb)
-            acc[b][mb][nb] = (p.dbg & 2) ? acc[b][mb][nb] + (float)cur[nb][0] * (float)xf[mb][ks][1]
-                                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[nb], xf[mb][ks], acc[b][mb][nb], 0, 0, 0);
+            if constexpr (DBG & 2) asm volatile("" ::"v"(cur[nb]), "v"(xf[mb][ks]));
+            else acc[b][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[nb], xf[mb][ks], acc[b][mb][nb], 0, 0, 0);
         // previous tile's epilogue, one part every other K-step, under these MFMAs
-        if (j > 0 && ks % 2 == 1 && ks / 2 < 2 * kXsMB && !(p.dbg & 1)) epi_part(b ^ 1, t - 1, ks / 2);
+        if (!first && ks % 2 == 1 && ks / 2 < 2 * kXsMB && !(DBG & 1)) epi_part(b ^ 1, t - 1, ks / 2);
+        if constexpr (DBG & 8) {   // the next step's W reads first, then the MFMAs with the epilogue's VALU between
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+          for (int i = 0; i < 2 * kXsMB * 2; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    for (int j = 0; j < n; j += 2) {
-      tile(std::integral_constant<int, 0>{}, j);
-      if (j + 1 < n) tile(std::integral_constant<int, 1>{}, j + 1);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    tile(I0{}, std::true_type{}, 0);
+    for (int j = 1; j < n; j += 2) {
+      tile(I1{}, std::false_type{}, j);
+      if (j + 1 < n) tile(I0{}, std::false_type{}, j + 1);
     }
     if ((n - 1) & 1) {
 #pragma unroll
@@ -221,8 +242,26 @@ hipError_t launch_xs(const GemmArgs& a, int nc, hipStream_t st) {
   int grid = 256;
   const int need = (items + 7) / 8 * 8;
   if (grid > need) grid = need;
-  if (a.rowscale) hipLaunchKernelGGL((gemm_xs_kernel<EPI, true>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
-  else hipLaunchKernelGGL((gemm_xs_kernel<EPI, false>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
+#ifdef XS_ABLATE
+  if constexpr (EPI == EPI_SWIGLU) {
+    switch (a.rowscale ? a.dbg : 0) {
+#define XS_D(d) case d: hipLaunchKernelGGL((gemm_xs_kernel<EPI, true, true, d>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc); return hipGetLastError();
+      XS_D(1) XS_D(2) XS_D(3) XS_D(4) XS_D(5) XS_D(6) XS_D(7) XS_D(8) XS_D(9) XS_D(23) XS_D(17) XS_D(55) XS_D(32) XS_D(39)
+#undef XS_D
+      default: break;
+    }
+  }
+#endif
+  constexpr bool kF32 = (EPI != EPI_STORE);   // fp32 output only for the paired epilogues (pw1 GLU -> dwconv)
+  if (a.c_bf16) {
+    if (a.rowscale) hipLaunchKernelGGL((gemm_xs_kernel<EPI, true, true>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
+    else hipLaunchKernelGGL((gemm_xs_kernel<EPI, false, true>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
+  } else if constexpr (kF32) {
+    if (a.rowscale) hipLaunchKernelGGL((gemm_xs_kernel<EPI, true, false>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
+    else hipLaunchKernelGGL((gemm_xs_kernel<EPI, false, false>), dim3(grid), dim3(kXsWaves * 64), 0, st, a, nc);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -235,15 +274,7 @@ hipError_t gemm_xs(const GemmArgs& a, int epi, int nc, hipStream_t st) {
     return hipErrorInvalidValue;
   if (epi == EPI_STORE && !a.c_bf16) return hipErrorInvalidValue;
   const int nwt = a.N / kXsBN, ntm = (a.M + kXsBM - 1) / kXsBM;
-  if (nc <= 0) {   // the run length with the best round efficiency (items / (256 * rounds)), >= 4 tiles preferred
-    double best = -1.0;
-    for (int c = nwt; c >= 1; --c) {
-      const int items = ntm * ((nwt + c - 1) / c);
-      const int rounds = (items + 255) / 256;
-      const double eff = (double)items / (256.0 * rounds) - (c < 4 ? 0.2 : 0.0) + 1e-3 * c;
-      if (eff > best) { best = eff; nc = c; }
-    }
-  }
+  if (nc <= 0) nc = xs_run_length(ntm, nwt);
   switch (epi) {
     case EPI_SWIGLU: return launch_xs<EPI_SWIGLU>(a, nc, st);
     case EPI_GLU: return launch_xs<EPI_GLU>(a, nc, st);

@@ -65,6 +65,20 @@ struct GemmArgs {
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
 
+// W tiles per work item of the X-stationary kernels (gemm_xs, gemm_xs8: one 256-row X block, one workgroup per
+// CU): the run length minimising rounds x (run + 3), 3 tiles being the per-item cost of loading the X fragments and
+// draining the last tile's epilogue; ties go to the longer run (profiles/r03_xs_route_sweep.jsonl)
+inline int xs_run_length(int x_blocks, int w_tiles, int cus = 256) {
+  int best = w_tiles;
+  int64_t best_cost = INT64_MAX;
+  for (int c = w_tiles; c >= 1; --c) {
+    const int64_t items = (int64_t)x_blocks * ((w_tiles + c - 1) / c);
+    const int64_t cost = (items + cus - 1) / cus * (c + 3);
+    if (cost < best_cost) { best_cost = cost; best = c; }
+  }
+  return best;
+}
+
 // ---- MXFP8 (TONE_PRECISION_FP8; gemm_mx.hip) --------------------------------------------------------
 // e4m3 values with one E8M0 scale per 32 consecutive values along K (OCP MX)
 struct MxArgs {
@@ -173,8 +187,8 @@ struct AttnArgs {
 };
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 
-// a9: depthwise causal conv k31 with carried state + folded BatchNorm + SiLU.
-hipError_t launch_dwconv(const float* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
+// a9: depthwise causal conv k31 with carried state + folded BatchNorm + SiLU; g and out bf16 when obf, else fp32.
+hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
                          int T, int B, hipStream_t st);
 
 // a11: reduction state + grouped conv (384->1536, k3, s2) -> y [B*5][1536]

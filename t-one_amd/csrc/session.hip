@@ -455,6 +455,12 @@ int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8,
   a.M = M;
   a.N = N;
   a.K = K;
+  // FFN up from 40 blocks of 256 rows: the X-stationary MXFP8 kernel (M = 40960: 110 vs 137 us, M = 10240: 34 vs
+  // 39; profiles/r03_xs_route_sweep.jsonl)
+  if (epi == EPI_SWIGLU && K == 384 && (M + 255) / 256 >= 40) {
+    LAUNCH(fam, gemm_xs8(a, epi, 0, st));
+    return TONE_OK;
+  }
   LAUNCH(fam, gemm_mx(a, epi, st));
   return TONE_OK;
 }
@@ -587,7 +593,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     LAUNCH("attention", launch_attention(aa, st));
     CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
     // Convolution module (conformer_blocks.py:827-830)
-    CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true));
+    CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true,
+                   true));   // g in bf16 in the bf16 / fp8 modes (fp32 in fp32 mode: gemm_call drops c_bf16 there)
     LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st));
     CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
     // FFN2 + norm_out (conformer_blocks.py:832-836)
