@@ -802,8 +802,6 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
   // K = 384 paired projections from 40 (SwiGLU) / 60 (GLU) blocks of 256 rows up: the X-stationary kernel
   // (FFN up M = 40960: 114 vs 165 us, M = 10240: 37 vs 41; pw1 M = 40960: 42 vs 47; profiles/r03_xs_route_sweep.jsonl)
-  // N = 384 residual projections: whole-row tiles (A read once; the fused norm_out needs whole rows)
-  if (epi == EPI_RESID && a.N == 384 && (a.norm_w || gemm_rows_route(a.M, a.K))) return gemm_rows(a, a.norm_w, 0, st);
   const int xblocks = (a.M + 255) / 256;
   if (a.K == 384 && ((epi == EPI_SWIGLU && xblocks >= 40) || (epi == EPI_GLU && xblocks >= 60))) {
     const hipError_t e = gemm_xs(a, epi, 0, st);

@@ -61,8 +61,6 @@ struct GemmArgs {
   int prio;           // bf16 kernels: static priority for the second half of the waves (set by gemm(), TONE_PRIO_BF16)
   int xcd_a;          // gemm_x3: XCD x owns the 2D tile block (n-group x % a, m-group x / a) of an a x (8 / a)
                       // split (set by the launcher; 0 = the default order)
-  const float* norm_w; // RESID, bf16 operands: the output rows RMS-normalised with this weight in the epilogue
-                       // (gemm_rows only; the caller checks gemm_rows_route first)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -119,13 +117,6 @@ hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // X-stationary bf16 GEMM for K = 384 (gemm_xs.hip): X rows in registers, W tiles streamed through an LDS ring,
 // epilogue overlapped with the next tile's MFMAs; SWIGLU / GLU / STORE (bf16 out); nc = W tiles per work item (0: auto)
 hipError_t gemm_xs(const GemmArgs& a, int epi, int nc, hipStream_t st);
-// full-row bf16 GEMM for N = 384 RESID projections (gemm_rows.hip): C = R + alpha (A W^T + bias) and its bf16 shadow
-// C2; norm_w (optional): the output rows RMS-normalised with weight norm_w (norm_out fused); mb = 16-row blocks per
-// tile (0: gemm_rows_mb(M))
-hipError_t gemm_rows(const GemmArgs& a, const float* norm_w, int mb, hipStream_t st);
-int gemm_rows_mb(int M);
-// whether gemm() sends an N = 384 RESID GEMM of M rows and depth K (bf16 operands) to gemm_rows
-bool gemm_rows_route(int M, int K);
 // exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3
