@@ -9,7 +9,8 @@ root, prec, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
 PAT = {  # SWIGLU instantiations: EPI_SWIGLU = 2
     "fp32": re.compile(r"gemm_x3_kernel<.*XT<\d+, \d+, \d+, \d+, \d+, \d+>, 2, (true|false), (true|false)(, (true|false))*>"),
     "fp32-mfma": re.compile(r"gemm_kernel<tone::Tile<\d+, \d+, \d+, \d+>, 2,"),
-    "bf16": re.compile(r"gemm_t_kernel<.*TT<\d+, \d+, \d+, \d+>, 2, (true|false)>"),
+    "bf16": re.compile(r"(gemm_t_kernel<.*TT<\d+, \d+, \d+, \d+>, 2, (true|false)>|gemm_xs_kernel<2, )"),
+    "fp8": re.compile(r"(gemm_xs8_kernel<2, |gemm_mx_kernel<\d+, 2, )"),
 }[prec]
 
 
