@@ -407,7 +407,9 @@ constexpr int kX8K = 384, kX8KS = kX8K / 128, kX8BM = 256, kX8BN = 64, kX8Tile =
 constexpr int kX8Pieces = kX8Tile / 1024 / 8;   // 3
 constexpr int kX8MaxN = 3072;
 
-template <int EPI, bool RS>
+// DBG (XS8_ABLATE microbenchmark builds only): 1 no epilogue, 2 no MFMA, 4 no W DMA after the prologue, 8 SwiGLU
+// without the MX quantization (raw bits stored)
+template <int EPI, bool RS, int DBG = 0>
 __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_STORE, "SWIGLU / STORE");
   constexpr int kStores8 = EPI == EPI_SWIGLU ? 2 * 3 : 4 * 2;      // vector stores per tile epilogue (per lane)
@@ -483,12 +485,18 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           }
         }
         float am = 0.f;
+        int e = 0;
+        u32x2 qv;
+        if constexpr (DBG & 8) {
+          qv = u32x2{__float_as_uint(v[0] + v[1] + v[2] + v[3]), __float_as_uint(v[4] + v[5] + v[6] + v[7])};
+        } else {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
-        am = fmaxf(am, __shfl_xor(am, 16, 64));
-        am = fmaxf(am, __shfl_xor(am, 32, 64));
-        const int e = mx_exp(am);
-        const u32x2 qv = quant8(v, exp2i(e));
+          for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
+          am = fmaxf(am, __shfl_xor(am, 16, 64));
+          am = fmaxf(am, __shfl_xor(am, 32, 64));
+          e = mx_exp(am);
+          qv = quant8(v, exp2i(e));
+        }
         const int col = 32 * t;                                   // first h column of the block
         *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 4 * lg) = qv[0];
         *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 16 + 4 * lg) = qv[1];
@@ -517,7 +525,7 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       const int t = t0 + j;
       vmcnt_dyn(ring_younger(j, n, kX8R, kX8Pieces, kStores8));   // tile t landed
       barrier_lds();                                              // ... for every wave; slot (t - 1) % R free
-      if (j + kX8R - 1 < n) dma(t + kX8R - 1);
+      if (j + kX8R - 1 < n && !(DBG & 4)) dma(t + kX8R - 1);
       const uint8_t* base = lds + (t % kX8R) * kX8Tile;
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
@@ -549,9 +557,10 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb)
-            acc[b][mb][nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[nb], xf[mb][ks], acc[b][mb][nb], 0, 0, 0,
-                                                                              ws[nb], 0, xs[mb][ks]);
-        if (j > 0) {                                              // previous tile, under these MFMAs
+            if constexpr (DBG & 2) asm volatile("" ::"v"(wf[nb]), "v"(xf[mb][ks]), "v"(ws[nb]), "v"(xs[mb][ks]));
+            else acc[b][mb][nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[nb], xf[mb][ks], acc[b][mb][nb],
+                                                                                   0, 0, 0, ws[nb], 0, xs[mb][ks]);
+        if (j > 0 && !(DBG & 1)) {                                // previous tile, under these MFMAs
           if (ks == 0) epi_part(b ^ 1, t - 1, 0);
           if (ks == 1) epi_part(b ^ 1, t - 1, 2);
           if (ks == 2) { epi_part(b ^ 1, t - 1, 1); epi_part(b ^ 1, t - 1, 3); }
@@ -563,7 +572,14 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       tile(std::integral_constant<int, 0>{}, j);
       if (j + 1 < n) tile(std::integral_constant<int, 1>{}, j + 1);
     }
-    if ((n - 1) & 1) {
+    if constexpr (DBG & 1) {   // keep the accumulators alive
+      float k = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) k += acc[0][mb][nb][0] + acc[1][mb][nb][1];
+      if (k == 1234.5f) p.C8[mbase] = 1;
+    } else if ((n - 1) & 1) {
 #pragma unroll
       for (int part = 0; part < 4; ++part) epi_part(1, t1 - 1, part);
     } else {
@@ -580,6 +596,16 @@ hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
   int grid = 256;
   const int need = (items + 7) / 8 * 8;
   if (grid > need) grid = need;
+#ifdef XS8_ABLATE
+  if constexpr (EPI == EPI_SWIGLU) {
+    switch (a.rs_inv ? a.dbg : 0) {
+#define X8_D(d) case d: hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true, d>), dim3(grid), dim3(512), 0, st, a, nc); return hipGetLastError();
+      X8_D(1) X8_D(2) X8_D(3) X8_D(4) X8_D(5) X8_D(8) X8_D(7)
+#undef X8_D
+      default: break;
+    }
+  }
+#endif
   if (a.rs_inv) hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true>), dim3(grid), dim3(512), 0, st, a, nc);
   else hipLaunchKernelGGL((gemm_xs8_kernel<EPI, false>), dim3(grid), dim3(512), 0, st, a, nc);
   return hipGetLastError();

@@ -16,6 +16,10 @@
 //     folded RMSNorm is summed from the X fragments during a step's first sub-tile;
 //   * the waves never meet again after the W load, so one wave's loads and epilogue run under the other SIMD
 //     wave's MFMAs.
+// Measured (tools/gemm_bench, profiles/r03_ws_sweep.jsonl, r03_ws_ablate.jsonl): equal to gemm_xs at M = 40960
+// (123 vs 125 us), slower at M <= 20480; its ablations show the MFMAs (~53 us at the 32x32x16 shape's sustained
+// 1.8 PF), the W fragment reads (~31) and the X loads (~16) adding up rather than overlapping.  Kept out of
+// libtonehip.so; built into the microbenchmark only.
 // Work split: N / 192 n-groups x (256 / n-groups) m-groups, one workgroup per CU; the workgroups of one m-group
 // (same X rows, different W slices) sit on one XCD, so each X row comes from HBM once per launch and from that
 // XCD's L2 for the other n-groups.  W is read from HBM/MALL once per XCD.

@@ -117,8 +117,9 @@ hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // X-stationary bf16 GEMM for K = 384 (gemm_xs.hip): X rows in registers, W tiles streamed through an LDS ring,
 // epilogue overlapped with the next tile's MFMAs; SWIGLU / GLU / STORE (bf16 out); nc = W tiles per work item (0: auto)
 hipError_t gemm_xs(const GemmArgs& a, int epi, int nc, hipStream_t st);
-// W-stationary bf16 GEMM for K = 384 (gemm_ws.hip): a 192-row W slice per workgroup held in LDS for the whole launch,
-// X streamed by each wave straight into registers; SWIGLU / GLU / STORE; variant 0 / 1 (see there)
+// W-stationary bf16 GEMM for K = 384 (gemm_ws.hip, microbenchmark build only -- measured no faster than gemm_xs,
+// DESIGN.md section 3): a 192-row W slice per workgroup held in LDS for the whole launch, X streamed by each wave
+// straight into registers; SWIGLU / GLU / STORE; variant 0 / 1 (see there)
 hipError_t gemm_ws(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
