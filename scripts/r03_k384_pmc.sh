@@ -10,9 +10,9 @@ for v in "xs 0" "xs 2" "xs8 0" "xs8 2"; do
   d=gpurun_out/k384_pmc_$1_$2
   rm -rf $d
   if [ $1 = xs ]; then
-    timeout -s KILL 60 rocprofv3 --pmc $C -d $d -o run --output-format csv -- env ROWSCALE=1 XSDBG=$2 $A 40960 384 3072 2 -10 1 5 > $d.log 2>&1 || exit $?
+    ROWSCALE=1 XSDBG=$2 timeout -s KILL 60 rocprofv3 --pmc $C -d $d -o run --output-format csv -- $A 40960 384 3072 2 -10 1 5 > $d.log 2>&1 || exit $?
   else
-    timeout -s KILL 60 rocprofv3 --pmc $C -d $d -o run --output-format csv -- env ROWSCALE=1 MXDBG=$2 $A 40960 384 3072 2 98 1 5 > $d.log 2>&1 || exit $?
+    ROWSCALE=1 MXDBG=$2 timeout -s KILL 60 rocprofv3 --pmc $C -d $d -o run --output-format csv -- $A 40960 384 3072 2 98 1 5 > $d.log 2>&1 || exit $?
   fi
   echo "$v ok"
 done
