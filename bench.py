@@ -391,6 +391,9 @@ def main() -> None:
     ap.add_argument("--config5", type=int, default=4096,
                     help="also measure BASELINE config 5's device step: this many streams sharded over the N GPUs, "
                          "MXFP8 q/k/v + FFN GEMMs, logprobs all-gathered (0 = skip)")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="initialise the process group even at N = 1 (torchrun --nproc-per-node 1): the weight broadcast, "
+                         "the per-step logprob all-gather and the max-over-ranks reduction then run through RCCL on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -403,7 +406,7 @@ def main() -> None:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
-    if world > 1:
+    if world > 1 or args.dist_always:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -485,7 +488,7 @@ def main() -> None:
             "config": {"workload": wl, "model": "T-one 71.7M (16-layer chunked Conformer, d384)",
                        "batch_per_gpu": cap, "global_batch": total, "chunk_ms": 300,
                        "parallelism": f"dp{world}", "graph": not args.no_graph,
-                       "collective": "RCCL all_gather_into_tensor of logprobs per step, overlapped" if world > 1
+                       "collective": "RCCL all_gather_into_tensor of logprobs per step, overlapped" if pg is not None
                        else None},
             "chunks_per_s": round(chunks_s, 1),
             "rtf": round(ms_step / 300.0, 5),

@@ -22,8 +22,8 @@ def _port() -> int:
     return p
 
 
-def _torchrun(args, timeout):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+def _torchrun(args, timeout, nproc=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     env = dict(os.environ, OMP_NUM_THREADS="4")
     return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
@@ -55,3 +55,21 @@ def test_bench_world2_strong_scaling_rehearsal():
     c4, c5 = out["alt_workloads"]
     assert c4["global_batch"] == 32 and c4["batch_per_gpu"] == 16 and c4["scaling"] == "strong"
     assert c5["dtype"] == "fp8" and c5["batch_per_gpu"] == 16 and c5["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world1():
+    """bench.py's collective path through RCCL itself (the nccl backend) on the box's one GPU: world size 1, so the
+    weight broadcast, the double-buffered logprob all-gather on the comm stream and the max-over-ranks all_reduce
+    run as real RCCL calls (two ranks would need two cards)."""
+    r = _torchrun(["bench.py", "--gpus", "1", "--dist-always", "--dist-backend", "nccl", "--steps", "6", "--warmup", "2",
+                   "--alt", "0", "--config4", "64", "--config5", "64", "--cpu-baseline-s", "0", "--batch", "64"],
+                  timeout=240, nproc=1)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["value"] > 0
+    assert out["config"]["collective"] and "RCCL" in out["config"]["collective"]
+    c4, c5 = out["alt_workloads"]
+    assert c4["value"] > 0 and c5["value"] > 0 and c5["dtype"] == "fp8"
