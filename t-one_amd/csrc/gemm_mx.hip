@@ -408,7 +408,8 @@ constexpr int kX8Pieces = kX8Tile / 1024 / 8;   // 3
 constexpr int kX8MaxN = 3072;
 
 // DBG (XS8_ABLATE microbenchmark builds only): 1 no epilogue, 2 no MFMA, 4 no W DMA after the prologue, 8 SwiGLU
-// without the MX quantization (raw bits stored)
+// without the MX quantization (raw bits stored), 16 no workgroup barrier per W tile (wrong results: timing only),
+// 32 static priority for waves 4-7, 64 / 128 W fragment schedules (see the tile loop)
 template <int EPI, bool RS, int DBG = 0>
 __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_STORE, "SWIGLU / STORE");
@@ -419,6 +420,9 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lg = lane >> 4, swz = (l15 >> 1) & 7;
+  if constexpr ((DBG & 32) != 0) {
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   const int nwt = p.N / kX8BN, ntm = (p.M + kX8BM - 1) / kX8BM, nch = (nwt + nc - 1) / nc;
   const int items = ntm * nch;
   const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
@@ -467,10 +471,17 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
     }
 
     f32x4 acc[2][2][4];   // [buffer][mb][nb]
+    // output row offsets of this lane's two rows (32-bit, from the uniform bases; every lane stores -- fixed count
+    // per tile for the counted vmcnt -- and a row past M rewrites row M - 1's values)
+    uint32_t orow[2], srow[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const uint32_t mrow = (uint32_t)min(mbase + 16 * mb + l15, p.M - 1);
+      orow[mb] = mrow * (uint32_t)p.ldc;
+      srow[mb] = mrow * (uint32_t)p.ldc8s;
+    }
     auto epi_part = [&](int b, int t, int part) __attribute__((always_inline)) {
       const int mb = part >> 1, hh = part & 1;
-      // every lane stores (fixed count per tile for the counted vmcnt): a row past M rewrites row M - 1's values
-      const int64_t mrow = min(mbase + 16 * mb + l15, p.M - 1);
       if constexpr (EPI == EPI_SWIGLU) {
         if (hh) return;                       // one MX block (32 h columns) per row and tile: both halves here
         float v[8];
@@ -498,9 +509,10 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           qv = quant8(v, exp2i(e));
         }
         const int col = 32 * t;                                   // first h column of the block
-        *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 4 * lg) = qv[0];
-        *reinterpret_cast<uint32_t*>(p.C8 + mrow * p.ldc + col + 16 + 4 * lg) = qv[1];
-        p.C8s[mrow * p.ldc8s + t] = (uint8_t)e;                   // the 4 lanes of the block write the same byte
+        uint8_t* c8 = p.C8 + orow[mb] + (col + 4 * lg);
+        *reinterpret_cast<uint32_t*>(c8) = qv[0];
+        *reinterpret_cast<uint32_t*>(c8 + 16) = qv[1];
+        p.C8s[srow[mb] + t] = (uint8_t)e;                         // the 4 lanes of the block write the same byte
       } else {
 #pragma unroll
         for (int nb2 = 0; nb2 < 2; ++nb2) {
@@ -511,7 +523,7 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           const __bf16 b0 = (__bf16)o[0], b1 = (__bf16)o[1], b2 = (__bf16)o[2], b3 = (__bf16)o[3];
           const u32x2 w = {(uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16),
                            (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16)};
-          *reinterpret_cast<u32x2*>(static_cast<uint16_t*>(p.C) + mrow * p.ldc + col) = w;
+          *reinterpret_cast<u32x2*>(static_cast<uint16_t*>(p.C) + orow[mb] + col) = w;
         }
       }
     };
@@ -524,7 +536,8 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       constexpr int b = decltype(Bc)::value;
       const int t = t0 + j;
       vmcnt_dyn(ring_younger(j, n, kX8R, kX8Pieces, kStores8));   // tile t landed
-      barrier_lds();                                              // ... for every wave; slot (t - 1) % R free
+      if constexpr (!(DBG & 16)) barrier_lds();                   // ... for every wave; slot (t - 1) % R free
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (j + kX8R - 1 < n && !(DBG & 4)) dma(t + kX8R - 1);
       const uint8_t* base = lds + (t % kX8R) * kX8Tile;
 #pragma unroll
@@ -542,16 +555,24 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           ws[nb] = sWs[(t * kX8BN + row) * (kX8K / 32) + 4 * ks + lg];
         }
       };
-      i32x8 wa[4], wb[4];
-      int sa[4], sbw[4];
-      rdw(0, wa, sa);
+      // W fragments: K-steps 0 and 1 requested right after the barrier (two register slots), K-step 2 into slot 0
+      // as soon as K-step 0's MFMAs have read it -- K-step 1 never waits on an LDS round trip of its own.
+      // DBG 64: one K-step ahead (the earlier schedule); DBG 128: all three K-steps at the barrier (3 slots, spills)
+      constexpr int kSlots = (DBG & 128) ? 3 : 2;
+      i32x8 wfa[kSlots][4];
+      int wsa[kSlots][4];
+      if constexpr ((DBG & 64) != 0) {
+        rdw(0, wfa[0], wsa[0]);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < kSlots; ++ks) rdw(ks, wfa[ks], wsa[ks]);
+      }
 #pragma unroll
       for (int ks = 0; ks < kX8KS; ++ks) {
-        i32x8(&wf)[4] = (ks & 1) ? wb : wa;
-        int(&ws)[4] = (ks & 1) ? sbw : sa;
-        if (ks + 1 < kX8KS) {
-          if (ks & 1) rdw(ks + 1, wa, sa);
-          else rdw(ks + 1, wb, sbw);
+        i32x8(&wf)[4] = wfa[ks % kSlots];
+        int(&ws)[4] = wsa[ks % kSlots];
+        if constexpr ((DBG & 64) != 0) {
+          if (ks + 1 < kX8KS) rdw(ks + 1, wfa[(ks + 1) % kSlots], wsa[(ks + 1) % kSlots]);
         }
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
@@ -560,6 +581,9 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
             if constexpr (DBG & 2) asm volatile("" ::"v"(wf[nb]), "v"(xf[mb][ks]), "v"(ws[nb]), "v"(xs[mb][ks]));
             else acc[b][mb][nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[nb], xf[mb][ks], acc[b][mb][nb],
                                                                                    0, 0, 0, ws[nb], 0, xs[mb][ks]);
+        if constexpr (kSlots == 2 && !(DBG & 64)) {
+          if (ks == 0) rdw(2, wfa[0], wsa[0]);
+        }
         if (j > 0 && !(DBG & 1)) {                                // previous tile, under these MFMAs
           if (ks == 0) epi_part(b ^ 1, t - 1, 0);
           if (ks == 1) epi_part(b ^ 1, t - 1, 2);
@@ -600,7 +624,7 @@ hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
   if constexpr (EPI == EPI_SWIGLU) {
     switch (a.rs_inv ? a.dbg : 0) {
 #define X8_D(d) case d: hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true, d>), dim3(grid), dim3(512), 0, st, a, nc); return hipGetLastError();
-      X8_D(1) X8_D(2) X8_D(3) X8_D(4) X8_D(5) X8_D(8) X8_D(7)
+      X8_D(1) X8_D(2) X8_D(3) X8_D(4) X8_D(5) X8_D(8) X8_D(7) X8_D(16) X8_D(17) X8_D(32) X8_D(20) X8_D(64) X8_D(65) X8_D(128)
 #undef X8_D
       default: break;
     }
@@ -618,6 +642,7 @@ hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st) {
   if (a.K != kX8K || a.N % kX8BN || a.N > kX8MaxN || a.M <= 0 || a.lda % 16 || a.ldas != kX8K / 32 || a.C2)
     return hipErrorInvalidValue;
   if (epi == EPI_SWIGLU && (!a.C8 || !a.C8s || a.ldc % 16)) return hipErrorInvalidValue;
+  if ((int64_t)a.M * a.ldc >= (1ll << 32) || (int64_t)a.M * a.ldc8s >= (1ll << 32)) return hipErrorInvalidValue;   // 32-bit row offsets
   if (epi == EPI_STORE && (!a.c_bf16 || a.ldc % 8)) return hipErrorInvalidValue;
   const int nwt = a.N / kX8BN, ntm = (a.M + kX8BM - 1) / kX8BM;
   if (nc <= 0) nc = xs_run_length(ntm, nwt);
