@@ -900,6 +900,22 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     // step the ring kernel is slower (profiles/r02_r3_sweep.jsonl)
     if (epi == EPI_STORE && a.N == 768 && a.M >= 4096 && a.W && !a.rowscale)
       return gemm_r3(a, epi, a.M >= 8192 ? 0 : 1, st);
+    // a few rows (B <= 6 streams: the drop-in's per-call batch): the launch is bound by streaming W through the
+    // few workgroups' LDS, so spread W over more of them (profiles/r03_b1_sweep.jsonl, M = 10 / 5): FFN up on
+    // 128x64 four-wave tiles (16.6 vs 20.7 us), FFN down / the reduction 1x1 split four ways on 64x32 tiles (9.6 vs
+    // 15.0), the subsampling Linear (K = 2176) split four ways on 64x64 four-wave tiles (16.9 vs 19.1), the other
+    // N = 384 / 1152 projections on 64x32 tiles (6.5 vs 6.8, 7.2 vs 18.6)
+    if (a.M <= 64) {
+      if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 5, st);
+      if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) {
+        if (a.K >= 1024 && !a.rowscale && a.ws && a.K % 4 == 0 && (int64_t)4 * a.M * a.N <= a.ws_cap &&
+            !a.c_plane && !a.c2_plane) {
+          const hipError_t e = gemm_x3_splitk(a, epi, a.K >= 2048 ? 4 : 9, 4, st);
+          if (e != hipErrorInvalidValue) return e;
+        }
+        return gemm_x3(a, epi, 9, st);
+      }
+    }
     if (epi == EPI_SWIGLU && a.N % 256 == 0)
       return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200 ? 7 : 6, st);
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);

@@ -36,8 +36,9 @@ def test_world2_sessions_gather_matches_single_process(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(out.read_text())
     assert res["world"] == 2 and res["shape"] == [7, 10, 35]
-    # the gathered shards equal the one-process batch (streams are independent; same kernels)
-    assert res["d_single"] <= 1e-5, res
+    # the gathered shards equal the one-process batch up to summation order: streams are independent, but the GEMM
+    # routing depends on the row count (3-4 streams per rank = M <= 64 routes to the small-M tiles, 7 streams does not)
+    assert res["d_single"] <= 1e-4, res
     assert res["d_oracle"] < 1e-3, res
 
 
