@@ -116,18 +116,28 @@ __device__ __forceinline__ void vmcnt_dyn(int n) {
 // i - 1): the number of this wave's vector-memory ops issued after tile j's DMA, i.e. the vmcnt that guarantees
 // tile j landed.  (Ops the compiler adds only make the wait stricter.)
 __device__ __forceinline__ int ring_younger(int j, int n, int R, int P, int S) {
-  int c = 0;
-  int i0;
-  if (j <= R - 2) {
-    for (int t = j + 1; t <= R - 2; ++t) c += (t < n) ? P : 0;   // later prologue tiles
-    i0 = 0;
-  } else {
-    i0 = j - R + 1;                                            // the iteration that issued tile j ...
-    c += (i0 >= 1) ? S : 0;                                    // ... and its stores after it
-    ++i0;
-  }
-  for (int i = i0; i < j; ++i) c += ((i + R - 1 < n) ? P : 0) + ((i >= 1) ? S : 0);
-  return c;
+  // closed form (checked against the iteration-by-iteration count for R 2-6, P 1-12, S 0-8, n 1-40, every j): the
+  // loop form compiled to ~300 scalar instructions and branches per tile, enough to make the scalar unit a bottleneck
+  // of the K = 384 kernels.  DMAs after tile j's: prologue tiles j+1 .. min(R-2, n-1) (only when j <= R-2) and the
+  // in-loop DMAs of iterations a .. j-1 whose tile i+R-1 exists; stores: iterations max(1, a) .. j-1, plus the
+  // iteration that issued tile j (j - R + 1) when it is >= 1
+  const int pro = j <= R - 2 ? max(0, min(R - 2, n - 1) - j) : 0;
+  const int a = max(0, j - R + 2);
+  const int dm = max(0, min(j - 1, n - R) - a + 1);
+  const int st = max(0, j - max(1, a)) + (j >= R ? 1 : 0);
+  return (pro + dm) * P + st * S;
+}
+
+// The counted ring wait: the steady-state count (R - 2 later DMAs, R - 1 store groups) is one compile-time wait; the
+// other counts (the first R and last R - 1 tiles of a run) go through vmcnt_dyn's switch, which compiles to a
+// branch tree of ~60 scalar instructions -- too many to run on every tile.
+template <int R, int P, int S>
+__device__ __forceinline__ void ring_wait(int j, int n) {
+  constexpr int kSteady = (R - 2) * P + (R - 1) * S;
+  static_assert(kSteady <= 63, "vmcnt field");
+  const int c = ring_younger(j, n, R, P, S);
+  if (c >= kSteady) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kSteady) : "memory");
+  else vmcnt_dyn(c);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

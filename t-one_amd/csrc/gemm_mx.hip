@@ -409,7 +409,7 @@ constexpr int kX8MaxN = 3072;
 
 // DBG (XS8_ABLATE microbenchmark builds only): 1 no epilogue, 2 no MFMA, 4 no W DMA after the prologue, 8 SwiGLU
 // without the MX quantization (raw bits stored), 16 no workgroup barrier per W tile (wrong results: timing only),
-// 32 static priority for waves 4-7, 64 / 128 W fragment schedules (see the tile loop)
+// 32 static priority for waves 4-7, 256 no W fragment reads, 512 no X loads (timing only)
 template <int EPI, bool RS, int DBG = 0>
 __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_STORE, "SWIGLU / STORE");
@@ -436,10 +436,15 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   auto dma = [&](int t) {
     uint8_t* base = lds + (t % kX8R) * kX8Tile;
     (void)base;
+    const uint8_t* wt = p.W + (int64_t)t * kX8Tile;               // uniform: the tile's first W row
+    // the lane's piece addresses are recomputed per call (a few VALU): hoisted out of the tile loop they were three
+    // 64-bit pointers the register allocator spilled, and every scratch reload drained vmcnt
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int i = 0; i < kX8Pieces; ++i) {
-      const int pc = wid * kX8Pieces + i, lin = pc * 64 + lane, row = lin / 24, slot = lin % 24;
-      const uint8_t* src = p.W + (int64_t)(t * kX8BN + row) * kX8K + ((slot ^ ((row >> 1) & 7)) << 4);
+      const int pc = wid * kX8Pieces + i, lin = pc * 64 + ln, row = lin / 24, slot = lin % 24;
+      const uint8_t* src = wt + (uint32_t)(row * kX8K + ((slot ^ ((row >> 1) & 7)) << 4));
 #if defined(__HIP_DEVICE_COMPILE__)
       __builtin_amdgcn_global_load_lds(src, base + pc * 1024, 16, 0, 0);
 #else
@@ -462,12 +467,17 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       const uint8_t* xr = p.A + row * p.lda;
 #pragma unroll
       for (int ks = 0; ks < kX8KS; ++ks) {
-        const u32x4 a = *reinterpret_cast<const u32x4*>(xr + 128 * ks + 16 * lg);
-        const u32x4 b = *reinterpret_cast<const u32x4*>(xr + 128 * ks + 64 + 16 * lg);
-        xf[mb][ks] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
-        xs[mb][ks] = p.As[row * p.ldas + 4 * ks + lg];
+        if constexpr ((DBG & 512) != 0) {   // no X loads (timing only)
+          xf[mb][ks] = i32x8{} + (int)(lane * 0x01010101u + ks + item);
+          xs[mb][ks] = 127;
+        } else {
+          const u32x4 a = *reinterpret_cast<const u32x4*>(xr + 128 * ks + 16 * lg);
+          const u32x4 b = *reinterpret_cast<const u32x4*>(xr + 128 * ks + 64 + 16 * lg);
+          xf[mb][ks] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+          xs[mb][ks] = p.As[row * p.ldas + 4 * ks + lg];
+        }
       }
-      inv[mb] = RS ? p.rs_inv[row] : 1.0f;
+      inv[mb] = RS && !(DBG & 512) ? p.rs_inv[row] : 1.0f;
     }
 
     f32x4 acc[2][2][4];   // [buffer][mb][nb]
@@ -532,84 +542,93 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
 #pragma unroll
     for (int s0 = 0; s0 < kX8R - 1; ++s0)
       if (s0 < n) dma(t0 + s0);
+    // W fragments of tile t, K-step ks (two register slots, wf / ws)
+    auto rdw = [&](int t, int ks, i32x8 (&wf)[4], int (&ws)[4]) __attribute__((always_inline)) {
+      if constexpr ((DBG & 256) != 0) {   // no W fragment reads from LDS (timing only)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) { wf[nb] = xf[nb & 1][ks]; ws[nb] = xs[nb & 1][ks]; }
+        return;
+      }
+      const uint8_t* base = lds + (t % kX8R) * kX8Tile;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int row = 16 * nb + l15;
+        const uint8_t* r = base + row * kX8K;
+        const u32x4 a = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + lg) ^ swz));
+        const u32x4 c = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + 4 + lg) ^ swz));
+        wf[nb] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)c[0], (int)c[1], (int)c[2], (int)c[3]};
+        ws[nb] = sWs[(t * kX8BN + row) * (kX8K / 32) + 4 * ks + lg];
+      }
+    };
+    // the 8 MFMAs of K-step ks into accumulator buffer BB
+    auto mstep = [&](auto Bc, int ks, const i32x8 (&wf)[4], const int (&ws)[4]) __attribute__((always_inline)) {
+      constexpr int bb = decltype(Bc)::value;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          if constexpr (DBG & 2) {
+            const i32x8 wv = wf[nb], xv = xf[mb][ks];
+            const int wsv = ws[nb], xsv = xs[mb][ks];
+            asm volatile("" ::"v"(wv), "v"(xv), "v"(wsv), "v"(xsv));
+          } else {
+            acc[bb][mb][nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[nb], xf[mb][ks], acc[bb][mb][nb],
+                                                                               0, 0, 0, ws[nb], 0, xs[mb][ks]);
+          }
+    };
+    // Tile t in buffer b: its K-step 2 is deferred into the next tile's iteration, so the first LDS reads after
+    // each barrier (tile t's K-step 0 fragments) are in flight under the previous tile's last eight MFMAs instead of
+    // in front of an idle matrix pipe.  Fragment slots: tile t's K-step 0 / 2 in slot b, K-step 1 in slot b ^ 1 (which
+    // held the previous tile's deferred K-step 2 until its MFMAs were issued).  The stores per iteration (the
+    // previous tile's epilogue) are unchanged, so ring_younger's count holds.
+    i32x8 wslot[2][4];
+    int sslot[2][4];
     auto tile = [&](auto Bc, int j) __attribute__((always_inline)) {
       constexpr int b = decltype(Bc)::value;
+      using PB = std::integral_constant<int, b ^ 1>;
       const int t = t0 + j;
-      vmcnt_dyn(ring_younger(j, n, kX8R, kX8Pieces, kStores8));   // tile t landed
+      ring_wait<kX8R, kX8Pieces, kStores8>(j, n);                   // tile t landed
       if constexpr (!(DBG & 16)) barrier_lds();                   // ... for every wave; slot (t - 1) % R free
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (j + kX8R - 1 < n && !(DBG & 4)) dma(t + kX8R - 1);
-      const uint8_t* base = lds + (t % kX8R) * kX8Tile;
+      rdw(t, 0, wslot[b], sslot[b]);
+      if (j > 0) mstep(PB{}, 2, wslot[b ^ 1], sslot[b ^ 1]);      // the previous tile's deferred K-step
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) acc[b][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      auto rdw = [&](int ks, i32x8 (&wf)[4], int (&ws)[4]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) {
-          const int row = 16 * nb + l15;
-          const uint8_t* r = base + row * kX8K;
-          const u32x4 a = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + lg) ^ swz));
-          const u32x4 c = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + 4 + lg) ^ swz));
-          wf[nb] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)c[0], (int)c[1], (int)c[2], (int)c[3]};
-          ws[nb] = sWs[(t * kX8BN + row) * (kX8K / 32) + 4 * ks + lg];
-        }
-      };
-      // W fragments: K-steps 0 and 1 requested right after the barrier (two register slots), K-step 2 into slot 0
-      // as soon as K-step 0's MFMAs have read it -- K-step 1 never waits on an LDS round trip of its own.
-      // DBG 64: one K-step ahead (the earlier schedule); DBG 128: all three K-steps at the barrier (3 slots, spills)
-      constexpr int kSlots = (DBG & 128) ? 3 : 2;
-      i32x8 wfa[kSlots][4];
-      int wsa[kSlots][4];
-      if constexpr ((DBG & 64) != 0) {
-        rdw(0, wfa[0], wsa[0]);
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < kSlots; ++ks) rdw(ks, wfa[ks], wsa[ks]);
-      }
-#pragma unroll
-      for (int ks = 0; ks < kX8KS; ++ks) {
-        i32x8(&wf)[4] = wfa[ks % kSlots];
-        int(&ws)[4] = wsa[ks % kSlots];
-        if constexpr ((DBG & 64) != 0) {
-          if (ks + 1 < kX8KS) rdw(ks + 1, wfa[(ks + 1) % kSlots], wsa[(ks + 1) % kSlots]);
-        }
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
-            if constexpr (DBG & 2) asm volatile("" ::"v"(wf[nb]), "v"(xf[mb][ks]), "v"(ws[nb]), "v"(xs[mb][ks]));
-            else acc[b][mb][nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[nb], xf[mb][ks], acc[b][mb][nb],
-                                                                                   0, 0, 0, ws[nb], 0, xs[mb][ks]);
-        if constexpr (kSlots == 2 && !(DBG & 64)) {
-          if (ks == 0) rdw(2, wfa[0], wsa[0]);
-        }
-        if (j > 0 && !(DBG & 1)) {                                // previous tile, under these MFMAs
-          if (ks == 0) epi_part(b ^ 1, t - 1, 0);
-          if (ks == 1) epi_part(b ^ 1, t - 1, 2);
-          if (ks == 2) { epi_part(b ^ 1, t - 1, 1); epi_part(b ^ 1, t - 1, 3); }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      rdw(t, 1, wslot[b ^ 1], sslot[b ^ 1]);
+      mstep(Bc, 0, wslot[b], sslot[b]);
+      if (j > 0 && !(DBG & 1)) epi_part(b ^ 1, t - 1, 0);         // previous tile, under these MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      rdw(t, 2, wslot[b], sslot[b]);
+      mstep(Bc, 1, wslot[b ^ 1], sslot[b ^ 1]);
+      if (j > 0 && !(DBG & 1)) { epi_part(b ^ 1, t - 1, 2); epi_part(b ^ 1, t - 1, 1); epi_part(b ^ 1, t - 1, 3); }
+      __builtin_amdgcn_sched_barrier(0);
     };
     for (int j = 0; j < n; j += 2) {
       tile(std::integral_constant<int, 0>{}, j);
       if (j + 1 < n) tile(std::integral_constant<int, 1>{}, j + 1);
     }
-    if constexpr (DBG & 1) {   // keep the accumulators alive
-      float k = 0.f;
+    // the last tile: its deferred K-step, then its epilogue
+    auto drain = [&](auto Bc) __attribute__((always_inline)) {
+      constexpr int b = decltype(Bc)::value;
+      mstep(Bc, 2, wslot[b], sslot[b]);
+      if constexpr (DBG & 1) {   // keep the accumulators alive
+        float k = 0.f;
 #pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
+        for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb) k += acc[0][mb][nb][0] + acc[1][mb][nb][1];
-      if (k == 1234.5f) p.C8[mbase] = 1;
-    } else if ((n - 1) & 1) {
+          for (int nb = 0; nb < 4; ++nb) k += acc[0][mb][nb][0] + acc[1][mb][nb][1];
+        if (k == 1234.5f) p.C8[mbase] = 1;
+      } else {
 #pragma unroll
-      for (int part = 0; part < 4; ++part) epi_part(1, t1 - 1, part);
-    } else {
-#pragma unroll
-      for (int part = 0; part < 4; ++part) epi_part(0, t1 - 1, part);
-    }
+        for (int part = 0; part < 4; ++part) epi_part(b, t1 - 1, part);
+      }
+    };
+    if ((n - 1) & 1) drain(std::integral_constant<int, 1>{});
+    else drain(std::integral_constant<int, 0>{});
     __syncthreads();
   }
 }
@@ -624,7 +643,7 @@ hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
   if constexpr (EPI == EPI_SWIGLU) {
     switch (a.rs_inv ? a.dbg : 0) {
 #define X8_D(d) case d: hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true, d>), dim3(grid), dim3(512), 0, st, a, nc); return hipGetLastError();
-      X8_D(1) X8_D(2) X8_D(3) X8_D(4) X8_D(5) X8_D(8) X8_D(7) X8_D(16) X8_D(17) X8_D(32) X8_D(20) X8_D(64) X8_D(65) X8_D(128)
+      X8_D(1) X8_D(2) X8_D(3) X8_D(4) X8_D(5) X8_D(8) X8_D(7) X8_D(16) X8_D(17) X8_D(32) X8_D(20) X8_D(259) X8_D(515) X8_D(771) X8_D(263) X8_D(19) X8_D(256) X8_D(512)
 #undef X8_D
       default: break;
     }

@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
       constexpr bool first = decltype(Fc)::value;
       const int t = t0 + j;
       // tile t landed (ring_younger: the ops issued after its DMA -- later DMAs and the fixed-count stores)
-      vmcnt_dyn(ring_younger(j, n, kXsR, kXsPieces, kStores));
+      ring_wait<kXsR, kXsPieces, kStores>(j, n);
       barrier_lds();                                              // ... for every wave; slot (t - 1) % R free
       if (j + 2 < n && !(DBG & 4)) dma(t + 2);                   // two tiles of lead
       const uint8_t* base = lds + (t % kXsR) * kXsTile;
