@@ -201,11 +201,23 @@ __global__ void __launch_bounds__(512) sub1_bf16_kernel(const float* __restrict_
     }
     *reinterpret_cast<uint4*>(xb + 8 * i) = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  for (int i = tid; i < 8 * kRows * kX1Cols; i += 512) {   // shifted bf16 copies
-    const int sh8 = i / (kRows * kX1Cols), r = (i / kX1Cols) % kRows, j = i % kX1Cols;
-    const float v = (j + sh8 < kMels) ? x1[r * kMels + j + sh8] : 0.f;
-    const __bf16 h = (__bf16)v;
-    xc[sh8 * kCopy + r * kX1Cols + j] = __builtin_bit_cast(uint16_t, h);
+  // shifted bf16 copies, 8 elements (one 16-byte LDS store) per item: 6-7 items per thread instead of 50 one-element
+  // ones with two integer divisions each
+  constexpr int kChunks = kX1Cols / 8;
+  static_assert(kX1Cols % 8 == 0 && kCopy % 8 == 0, "16-byte aligned copy rows");
+  for (int i = tid; i < 8 * kRows * kChunks; i += 512) {
+    const int sh8 = i / (kRows * kChunks), rem = i - sh8 * (kRows * kChunks), r = rem / kChunks;
+    const int j0 = (rem - r * kChunks) * 8;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e0 = j0 + 2 * q + sh8;
+      const float v0 = e0 < kMels ? x1[r * kMels + e0] : 0.f;
+      const float v1 = e0 + 1 < kMels ? x1[r * kMels + e0 + 1] : 0.f;
+      const __bf16 h0 = (__bf16)v0, h1 = (__bf16)v1;
+      w[q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    }
+    *reinterpret_cast<uint4*>(xc + sh8 * kCopy + r * kX1Cols + j0) = make_uint4(w[0], w[1], w[2], w[3]);
   }
   __syncthreads();                                        // x1 is dead from here: its space holds tbuf
   __half* st2out = s.out + orow + kOffSub2;
