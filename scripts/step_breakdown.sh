@@ -9,7 +9,7 @@ prof() {  # tag, bench args...
   rm -rf /tmp/st_$tag
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/st_$tag -o run -- \
     python bench.py --steps 5 --warmup 2 --cpu-baseline-s 0 --alt 0 --config4 0 --config5 0 "$@" > gpurun_out/st_$tag.log 2>&1
-  python scripts/step_trace.py "$(find /tmp/st_$tag -name '*kernel_trace.csv' | head -1)" > gpurun_out/step_$tag.txt
+  python scripts/step_trace.py "$(find /tmp/st_$tag -name '*kernel_trace.csv' | head -1)" ${SEQ:-} > gpurun_out/step_$tag.txt
 }
 if [ $# -gt 0 ]; then prof "$@"; exit 0; fi   # one custom leg: tag, bench args...
 prof fp32_b256
