@@ -99,13 +99,34 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
       for (int ip = 0; ip < TI / 2; ++ip) {
         const int nl = wn * WTN + 64 * ip;                   // g rows nl..nl+31, u rows nl+32..nl+63
         float o[16];
+        if (p.c_bf16) {
+          // bf16 output: v_exp_f32 / v_rcp_f32, value pairs (consecutive columns) as two-float vectors so the fused
+          // multiply-adds and products issue as v_pk_* with the scalar form's per-element roundings
+          typedef float f32x2e __attribute__((ext_vector_type(2)));
+          const f32x2e inv2 = {inv, inv};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int n = nl + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const float g = fmaf(acc[2 * ip][j][r], inv, sb[n]);
-          const float u = fmaf(acc[2 * ip + 1][j][r], inv, sb[n + 32]);
-          if (p.c_bf16) o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
-          else o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);   // fp32 output: IEEE exp/div
+          for (int r = 0; r < 16; r += 2) {
+            const int n = nl + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const f32x2e g = __builtin_elementwise_fma(f32x2e{acc[2 * ip][j][r], acc[2 * ip][j][r + 1]}, inv2,
+                                                       f32x2e{sb[n], sb[n + 1]});
+            const f32x2e u = __builtin_elementwise_fma(f32x2e{acc[2 * ip + 1][j][r], acc[2 * ip + 1][j][r + 1]}, inv2,
+                                                       f32x2e{sb[n + 32], sb[n + 33]});
+            const f32x2e z = (EPI == EPI_SWIGLU) ? g : u;
+            const f32x2e t = z * -1.4426950408889634f;
+            const f32x2e d = f32x2e{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
+            const f32x2e sg = f32x2e{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+            const f32x2e y = (EPI == EPI_SWIGLU) ? g * sg * u : g * sg;
+            o[r] = y.x;
+            o[r + 1] = y.y;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int n = nl + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const float g = fmaf(acc[2 * ip][j][r], inv, sb[n]);
+            const float u = fmaf(acc[2 * ip + 1][j][r], inv, sb[n + 32]);
+            o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);   // fp32 output: IEEE exp/div
+          }
         }
         if (p.c_bf16) {
           store_tile_bf16(static_cast<uint16_t*>(p.C) + mrow * p.ldc + (n0 + nl) / 2, o, lh, ok, p.nt_store != 0);

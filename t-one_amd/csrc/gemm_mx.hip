@@ -41,11 +41,11 @@ __device__ __forceinline__ float fsig(float x) {
 
 // v / 2^(E - 127) clamped to e4m3's range, two values packed into the low / high half of `w`; a NaN stays a
 // NaN (the conversion encodes it as e4m3 NaN) instead of being clamped to a finite value
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool HI>
 __device__ __forceinline__ uint32_t cvt_pk(float a, float b, float inv, uint32_t w) {
-  a = sat_e4m3(a * inv);
-  b = sat_e4m3(b * inv);
-  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, (int)w, HI);
+  const f32x2 p = f32x2{a, b} * inv;                         // one v_pk_mul_f32
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(p.x), sat_e4m3(p.y), (int)w, HI);
 }
 // 8 floats -> 8 e4m3 bytes with the block's inverse scale
 __device__ __forceinline__ u32x2 quant8(const float (&v)[8], float inv) {
@@ -494,15 +494,25 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       const int mb = part >> 1, hh = part & 1;
       if constexpr (EPI == EPI_SWIGLU) {
         if (hh) return;                       // one MX block (32 h columns) per row and tile: both halves here
+        // value pairs as two-float vectors so the fused multiply-adds and products issue as v_pk_* (the same
+        // per-element roundings as the scalar form)
         float v[8];
+        const f32x2 inv2 = {inv[mb], inv[mb]};
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
           const int ng = kX8BN * t + 16 * h2 + 4 * lg;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float gg = fmaf(acc[b][mb][h2][r], inv[mb], sb[ng + r]);
-            const float uu = fmaf(acc[b][mb][2 + h2][r], inv[mb], sb[ng + 32 + r]);
-            v[4 * h2 + r] = gg * fsig(gg) * uu;
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 ag = {acc[b][mb][h2][r], acc[b][mb][h2][r + 1]};
+            const f32x2 au = {acc[b][mb][2 + h2][r], acc[b][mb][2 + h2][r + 1]};
+            const f32x2 bg = {sb[ng + r], sb[ng + r + 1]}, bu = {sb[ng + 32 + r], sb[ng + 33 + r]};
+            const f32x2 gg = __builtin_elementwise_fma(ag, inv2, bg);
+            const f32x2 uu = __builtin_elementwise_fma(au, inv2, bu);
+            const f32x2 tt = gg * -1.4426950408889634f;
+            const f32x2 dd = f32x2{__builtin_amdgcn_exp2f(tt.x), __builtin_amdgcn_exp2f(tt.y)} + 1.0f;
+            const f32x2 oo = gg * f32x2{__builtin_amdgcn_rcpf(dd.x), __builtin_amdgcn_rcpf(dd.y)} * uu;
+            v[4 * h2 + r] = oo.x;
+            v[4 * h2 + r + 1] = oo.y;
           }
         }
         float am = 0.f;
@@ -542,6 +552,9 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
 #pragma unroll
     for (int s0 = 0; s0 < kX8R - 1; ++s0)
       if (s0 < n) dma(t0 + s0);
+    // lane-constant parts of the W fragment / scale addresses (row l15 of each 16-row n-block, chunk lg / 4 + lg)
+    const int xa0 = l15 * kX8K + 16 * (lg ^ swz), xa1 = l15 * kX8K + 16 * ((4 + lg) ^ swz);
+    const int xas = l15 * (kX8K / 32) + lg;
     // W fragments of tile t, K-step ks (two register slots, wf / ws)
     auto rdw = [&](int t, int ks, i32x8 (&wf)[4], int (&ws)[4]) __attribute__((always_inline)) {
       if constexpr ((DBG & 256) != 0) {   // no W fragment reads from LDS (timing only)
@@ -549,15 +562,17 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
         for (int nb = 0; nb < 4; ++nb) { wf[nb] = xf[nb & 1][ks]; ws[nb] = xs[nb & 1][ks]; }
         return;
       }
-      const uint8_t* base = lds + (t % kX8R) * kX8Tile;
+      // (8 ks + c) ^ swz = 8 ks + (c ^ swz) for swz < 8: one lane-constant address per half plus compile-time offsets
+      // (n-block, K-step) that fold into the ds_read immediates; the ring slot and the tile's scale rows are uniform
+      const uint8_t* b0 = lds + (t % kX8R) * kX8Tile + xa0;
+      const uint8_t* b1 = lds + (t % kX8R) * kX8Tile + xa1;
+      const uint8_t* bs = sWs + t * kX8BN * (kX8K / 32) + xas;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
-        const int row = 16 * nb + l15;
-        const uint8_t* r = base + row * kX8K;
-        const u32x4 a = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + lg) ^ swz));
-        const u32x4 c = *reinterpret_cast<const u32x4*>(r + 16 * ((8 * ks + 4 + lg) ^ swz));
+        const u32x4 a = *reinterpret_cast<const u32x4*>(b0 + nb * 16 * kX8K + 128 * ks);
+        const u32x4 c = *reinterpret_cast<const u32x4*>(b1 + nb * 16 * kX8K + 128 * ks);
         wf[nb] = i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)c[0], (int)c[1], (int)c[2], (int)c[3]};
-        ws[nb] = sWs[(t * kX8BN + row) * (kX8K / 32) + 4 * ks + lg];
+        ws[nb] = bs[nb * 16 * (kX8K / 32) + 4 * ks];
       }
     };
     // the 8 MFMAs of K-step ks into accumulator buffer BB

@@ -132,12 +132,24 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
       if constexpr (PAIRED) {
         // g rows 16 nb + 4 lg + r (nb = hh), u rows 32 + 16 nb + 4 lg + r -> output column 32 t + 16 hh + 4 lg + r
         const int ng = kXsBN * t + 16 * hh + 4 * lg;
+        // value pairs as two-float vectors: the fused multiply-adds and products issue as v_pk_* with the same
+        // per-element roundings as the scalar form
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
         float o[4];
+        const f32x2 inv2 = {inv[mb], inv[mb]};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = fmaf(acc[b][mb][hh][r], inv[mb], sbias[ng + r]);
-          const float u = fmaf(acc[b][mb][2 + hh][r], inv[mb], sbias[ng + 32 + r]);
-          o[r] = (EPI == EPI_SWIGLU) ? fast_silu(g) * u : g * fast_sigmoid(u);
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 g = __builtin_elementwise_fma(f32x2{acc[b][mb][hh][r], acc[b][mb][hh][r + 1]}, inv2,
+                                                    f32x2{sbias[ng + r], sbias[ng + r + 1]});
+          const f32x2 u = __builtin_elementwise_fma(f32x2{acc[b][mb][2 + hh][r], acc[b][mb][2 + hh][r + 1]}, inv2,
+                                                    f32x2{sbias[ng + 32 + r], sbias[ng + 33 + r]});
+          const f32x2 z = (EPI == EPI_SWIGLU) ? g : u;              // the sigmoid's argument
+          const f32x2 t = z * -1.4426950408889634f;
+          const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
+          const f32x2 sg = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+          const f32x2 y = (EPI == EPI_SWIGLU) ? g * sg * u : g * sg;
+          o[r] = y.x;
+          o[r + 1] = y.y;
         }
         const int col = 32 * t + 16 * hh + 4 * lg;
         if constexpr (OBF) {
