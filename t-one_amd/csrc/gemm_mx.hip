@@ -13,9 +13,9 @@
 // Structure as gemm_p_kernel (gemm_t.hip): transposed orientation D[n][m] = W[n] . X[m], persistent
 // XCD-contiguous tiles, BNW (256 | 128) W rows x 256 X rows, K-tile = 128 fp8 = one 128-byte line per
 // row, 16 KiB quarters staged by LDS-DMA into a two-stage ring, every fragment of a K-tile read in
-// its first two MFMA phases so the stage is free after the first barrier, counted vmcnt(4) keeping
-// two quarters of K-tile t+2 in flight across the barrier.  The tile's scales, bias and row factors
-// go to LDS at the tile's start.
+// its first two MFMA phases so the stage is free after the first barrier, the whole of K-tile t+2 issued
+// right after that barrier and kept in flight across the end-of-step wait (counted vmcnt).  The tile's
+// scales, bias and row factors go to LDS at the tile's start; tile positions advance once per K-tile.
 #include "common.h"
 #include "kernels.h"
 
@@ -143,16 +143,27 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   if (nmine <= 0) return;                                       // workgroup-uniform
   const int nk = p.K / BK, KB = p.K / 32, G = nmine * nk;
 
-  auto tile_of = [&](int u, int& m0, int& n0) {
-    const int t = tbeg + jb + (u / nk) * nxb;
-    m0 = (t / ntn) * BMX;
-    n0 = (t % ntn) * BNW;
+  // running position of a K-step (uniform scalars): K-tile kt of the workgroup's ti-th tile at (m0, n0).  The
+  // loop carries the positions of steps t, t + 1, t + 2 and advances the last once per step, so the tile
+  // index divisions run once per tile instead of once per DMA quarter (they were ~130 SALU per K-step)
+  struct Pos {
+    int kt, ti, m0, n0;
   };
-  // quarter j of K-tile u: W rows 128 j.. (j < NQW) or X rows 128 (j - NQW)..; pieces of 8 rows x 128 B
-  auto issue = [&](int u, int j) {
-    int m0, n0;
-    tile_of(u, m0, n0);
-    const int k0 = (u % nk) * BK;
+  auto pos_tile = [&](Pos& s) {
+    const int t = tbeg + jb + s.ti * nxb;
+    s.m0 = (t / ntn) * BMX;
+    s.n0 = (t % ntn) * BNW;
+  };
+  auto advance = [&](Pos& s) {
+    if (++s.kt == nk) {
+      s.kt = 0;
+      ++s.ti;
+      pos_tile(s);
+    }
+  };
+  // quarter j of K-step u (position s): W rows 128 j.. (j < NQW) or X rows 128 (j - NQW)..; pieces of 8 rows x 128 B
+  auto issue = [&](int u, const Pos& s, int j) {
+    const int m0 = s.m0, n0 = s.n0, k0 = s.kt * BK;
     uint8_t* dst = lds + (u & 1) * STG + j * QB;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -168,13 +179,12 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
 #endif
     }
   };
-  auto issue_kt = [&](int u, int from, int to) {   // quarters [from, to) of K-tile u (NQW + 2 per K-tile)
-    for (int j = from; j < to; ++j) issue(u, j);
+  auto issue_kt = [&](int u, const Pos& s, int from, int to) {   // quarters [from, to) of K-step u (NQW + XQ each)
+    for (int j = from; j < to; ++j) issue(u, s, j);
   };
   // per-tile side data: scales, bias, row factors (plain loads; at tile boundaries only)
-  auto load_side = [&](int u) {
-    int m0, n0;
-    tile_of(u, m0, n0);
+  auto load_side = [&](const Pos& s) {
+    const int m0 = s.m0, n0 = s.n0;
     for (int i = tid; i < BNW * KB; i += 512) {
       const int r = i / KB, c = i % KB;
       sW[r * kMxKB + c] = p.Ws[(int64_t)(n0 + r) * KB + c];
@@ -206,9 +216,8 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
-  auto epilogue = [&](int u) {
-    int m0, n0;
-    tile_of(u, m0, n0);
+  auto epilogue = [&](const Pos& s) {
+    const int m0 = s.m0, n0 = s.n0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int ml = xrow0 + 16 * j + l15, m = m0 + ml;
@@ -279,22 +288,32 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
     }
   };
 
+  Pos s0{0, 0, 0, 0};
+  pos_tile(s0);
+  Pos s1 = s0;
+  advance(s1);
+  Pos s2 = s1;
+  advance(s2);
   zero();
-  load_side(0);
+  load_side(s0);
   __syncthreads();                                              // side data visible; no DMA in flight yet
   constexpr int QPT = NQW + XQ;                                 // quarters per K-tile
   // prologue: K-tile 0 whole, the first half of K-tile 1's quarters
-  issue_kt(0, 0, QPT);
+  // E quarters of K-step t + 2 go out after the stage-freeing barrier of step t, the other QPT - E in the first
+  // two phases of step t + 1.  All of them (E = QPT): the X quarters, the ones that miss L2, get 1.5 steps of
+  // cover instead of one (FFN down M = 40960: 62.0 -> 60.3 us; profiles/r03_mx_resid_early.jsonl); DBG bit 64
+  // restores E = QPT / 2 for the A/B
+  constexpr int E = (DBG & 64) ? QPT / 2 : QPT;
+  issue_kt(0, s0, 0, QPT);
   if (G > 1) {
-    issue_kt(1, 0, QPT / 2);
-    if constexpr (QPT / 2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    issue_kt(1, s1, 0, E);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * E) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   barrier_lds();
   for (int t = 0; t < G; ++t) {
-    const int buf = t & 1, kt = t % nk;
+    const int buf = t & 1, kt = s0.kt;
     i32x8 xf[4], wa[TH], wb[TH];
     int xs[4], wsa[TH], wsb[TH];
     // phase 0: every X fragment + the first half of the W tiles
@@ -308,7 +327,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
       wa[i] = rd(wq, buf, i);
       wsa[i] = sW[(wrow0 + 16 * i + l15) * kMxKB + 4 * kt + lg];
     }
-    if (t + 1 < G) issue_kt(t + 1, QPT / 2, QPT / 2 + (QPT - QPT / 2 + 1) / 2);
+    if (t + 1 < G) issue_kt(t + 1, s1, E, E + (QPT - E + 1) / 2);
 #pragma unroll
     for (int i = 0; i < TH; ++i)
 #pragma unroll
@@ -321,7 +340,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
       wb[i] = rd(wq, buf, TH + i);
       wsb[i] = sW[(wrow0 + 16 * (TH + i) + l15) * kMxKB + 4 * kt + lg];
     }
-    if (t + 1 < G) issue_kt(t + 1, QPT / 2 + (QPT - QPT / 2 + 1) / 2, QPT);
+    if (t + 1 < G) issue_kt(t + 1, s1, E + (QPT - E + 1) / 2, QPT);
 #pragma unroll
     for (int i = 0; i < TH; ++i)
 #pragma unroll
@@ -330,7 +349,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
                               : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
     barrier_lds();                                              // every wave's reads of stage buf done
     // phase 2
-    if (t + 2 < G) issue_kt(t + 2, 0, (QPT / 2 + 1) / 2);
+    if (t + 2 < G) issue_kt(t + 2, s2, 0, (E + 1) / 2);
 #pragma unroll
     for (int i = 0; i < TH; ++i)
 #pragma unroll
@@ -338,17 +357,16 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
         acc[TH + i][j] = (DBG & 4) ? acc[TH + i][j] + (float)(wb[i][4] ^ xf[j][5] ^ wsb[i] ^ xs[j])
                                    : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
     // phase 3
-    if (t + 2 < G) issue_kt(t + 2, (QPT / 2 + 1) / 2, QPT / 2);
+    if (t + 2 < G) issue_kt(t + 2, s2, (E + 1) / 2, E);
 #pragma unroll
     for (int i = 0; i < TH; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[TH + i][j] = (DBG & 4) ? acc[TH + i][j] + (float)(wb[i][6] ^ xf[j][7] ^ wsb[i] ^ xs[j])
                                    : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[i], xf[j], acc[TH + i][j], 0, 0, 0, wsb[i], 0, xs[j]);
-    // K-tile t+1 landed; the first half of K-tile t+2's quarters (2 pieces each) stays in flight
+    // K-tile t+1 landed; the E quarters of K-tile t+2 (2 pieces each) stay in flight
     if (t + 2 < G) {
-      if constexpr (QPT / 2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * E) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -361,15 +379,18 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
           for (int j = 0; j < 4; ++j)   // never true (alpha is finite): keeps every accumulator live
             if (p.alpha == -1.2345e30f) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + 4 * (64 * (i * 4 + j) + lane)) = acc[i][j];
       } else {
-        epilogue(t);
+        epilogue(s0);
       }
       zero();
       if (t + 1 < G && !(DBG & 2)) {
         __syncthreads();                                        // every epilogue done with the side data
-        load_side(t + 1);
+        load_side(s1);
         __syncthreads();
       }
     }
+    s0 = s1;
+    s1 = s2;
+    advance(s2);
   }
 }
 
@@ -390,6 +411,19 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
       default: return hipErrorInvalidValue;
     }
   }
+#ifdef XS8_ABLATE
+  if constexpr (EPI == EPI_RESID) {   // K-loop / epilogue split of the fp8 FFN down (no epilogue; no MFMA; neither)
+    switch (a.dbg & 15) {
+      case 0: break;
+      case 1: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 1, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 4: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 4, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 5: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 5, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 8: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 64, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      case 9: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 65, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      default: return hipErrorInvalidValue;
+    }
+  }
+#endif
   if (a.rs_inv) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
   return hipGetLastError();

@@ -144,8 +144,15 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)N * K + 255) / 256)), dim3(256), 0, 0, W8, Ws, Wf, (int64_t)N, K);
   hipLaunchKernelGGL(ref_mx_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, Af, Wf, bias, R, rowscale ? inv : nullptr,
                      ref, M, N, K, epi);
+  // LDAPAD: X rows at a pitch of K + LDAPAD bytes (L2 channel spread of the row-strided K-tile reads)
+  const int pad = getenv("LDAPAD") ? atoi(getenv("LDAPAD")) : 0;
+  uint8_t* A8p = A8;
+  if (pad) {
+    CK(hipMalloc(&A8p, (size_t)M * (K + pad)));
+    CK(hipMemcpy2D(A8p, K + pad, A8, K, K, M, hipMemcpyDeviceToDevice));
+  }
   MxArgs a{};
-  a.A = A8; a.lda = K; a.As = As; a.ldas = K / 32; a.W = W8; a.Ws = Ws; a.rs_inv = rowscale ? inv : nullptr;
+  a.A = A8p; a.lda = K + pad; a.As = As; a.ldas = K / 32; a.W = W8; a.Ws = Ws; a.rs_inv = rowscale ? inv : nullptr;
   a.bias = bias; a.C = C; a.ldc = nout; a.c_bf16 = 0; a.R = R; a.ldr = N; a.alpha = 1.f;
   a.C8 = C8; a.C8s = C8s; a.ldc8s = nout / 32; a.M = M; a.N = N; a.K = K;
   a.dbg = getenv("MXDBG") ? atoi(getenv("MXDBG")) : 0;   // gemm_mx.hip DBG bits (SWIGLU only)
