@@ -163,6 +163,8 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   };
   // quarter j of K-step u (position s): W rows 128 j.. (j < NQW) or X rows 128 (j - NQW)..; pieces of 8 rows x 128 B
   auto issue = [&](int u, const Pos& s, int j) {
+    if constexpr ((DBG & 16) != 0)   // no DMA after the first two K-steps (timing only)
+      if (u >= 2) return;
     const int m0 = s.m0, n0 = s.n0, k0 = s.kt * BK;
     uint8_t* dst = lds + (u & 1) * STG + j * QB;
 #pragma unroll
@@ -182,26 +184,55 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   auto issue_kt = [&](int u, const Pos& s, int from, int to) {   // quarters [from, to) of K-step u (NQW + XQ each)
     for (int j = from; j < to; ++j) issue(u, s, j);
   };
-  // per-tile side data: scales, bias, row factors (plain loads; at tile boundaries only)
-  auto load_side = [&](const Pos& s) {
-    const int m0 = s.m0, n0 = s.n0;
-    for (int i = tid; i < BNW * KB; i += 512) {
-      const int r = i / KB, c = i % KB;
-      sW[r * kMxKB + c] = p.Ws[(int64_t)(n0 + r) * KB + c];
+  // per-tile side data: scales, bias, row factors (at tile boundaries only).  Fetched into registers as dwords,
+  // every load issued before any LDS store, the next tile's fetch ahead of this tile's epilogue: the byte-wise
+  // load/store loop it replaces cost ~5 us per tile boundary at M = 40960 (profiles/r03_mx_resid_ablate3.jsonl)
+  constexpr int XD = BMX * (kMxKB / 4) / 512, WD = (BNW * (kMxKB / 4) + 511) / 512;
+  struct Side {
+    uint32_t x[XD], w[WD];
+    float b, r;
+  };
+  auto side_fetch = [&](const Pos& s) {
+    const int m0 = s.m0, n0 = s.n0, nd = KB >> 2;   // dwords of scales per row
+    Side v;
+#pragma unroll
+    for (int q = 0; q < XD; ++q) {
+      const int i = tid + 512 * q, r = i / nd, c = i - r * nd;
+      v.x[q] = r < BMX ? *reinterpret_cast<const uint32_t*>(p.As + (int64_t)min(m0 + r, p.M - 1) * p.ldas + 4 * c) : 0u;
     }
-    for (int i = tid; i < BMX * KB; i += 512) {
-      const int r = i / KB, c = i % KB;
-      sX[r * kMxKB + c] = p.As[(int64_t)min(m0 + r, p.M - 1) * p.ldas + c];
+#pragma unroll
+    for (int q = 0; q < WD; ++q) {
+      const int i = tid + 512 * q, r = i / nd, c = i - r * nd;
+      v.w[q] = r < BNW ? *reinterpret_cast<const uint32_t*>(p.Ws + (int64_t)(n0 + r) * KB + 4 * c) : 0u;
     }
-    for (int i = tid; i < BNW; i += 512) sb[i] = p.bias ? p.bias[n0 + i] : 0.f;
-    if constexpr (RS)
-      for (int i = tid; i < BMX; i += 512) sr[i] = p.rs_inv[min(m0 + i, p.M - 1)];
+    v.b = (tid < BNW && p.bias) ? p.bias[n0 + tid] : 0.f;
+    v.r = (RS && tid < BMX) ? p.rs_inv[min(m0 + tid, p.M - 1)] : 1.f;
+    return v;
+  };
+  auto side_store = [&](const Side& v) {
+    const int nd = KB >> 2;
+#pragma unroll
+    for (int q = 0; q < XD; ++q) {
+      const int i = tid + 512 * q, r = i / nd, c = i - r * nd;
+      if (r < BMX) *reinterpret_cast<uint32_t*>(sX + r * kMxKB + 4 * c) = v.x[q];
+    }
+#pragma unroll
+    for (int q = 0; q < WD; ++q) {
+      const int i = tid + 512 * q, r = i / nd, c = i - r * nd;
+      if (r < BNW) *reinterpret_cast<uint32_t*>(sW + r * kMxKB + 4 * c) = v.w[q];
+    }
+    if (tid < BNW) sb[tid] = v.b;
+    if (RS && tid < BMX) sr[tid] = v.r;
   };
 
   const uint8_t* wq = lds + (wn * RW / 128) * QB + ((wn * RW) % 128) * BK;   // wave's W rows
   const uint8_t* xq = lds + (NQW + (wm >> 1)) * QB + (wm & 1) * 64 * BK;
   const int wrow0 = wn * RW, xrow0 = wm * 64;
   auto rd = [&](const uint8_t* qb, int buf, int tile) {
+    if constexpr ((DBG & 8) != 0) {   // no fragment reads from LDS (timing only)
+      const int v = (int)(intptr_t)qb ^ (buf << 4) ^ tile;
+      return i32x8{v, v, v, v, v, v, v, v};
+    }
     const uint8_t* r = qb + buf * STG + (16 * tile + l15) * BK;
     const u32x4 a = *reinterpret_cast<const u32x4*>(r + 16 * (lg ^ g));
     const u32x4 b = *reinterpret_cast<const u32x4*>(r + 16 * ((4 + lg) ^ g));
@@ -295,7 +326,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   Pos s2 = s1;
   advance(s2);
   zero();
-  load_side(s0);
+  side_store(side_fetch(s0));
   __syncthreads();                                              // side data visible; no DMA in flight yet
   constexpr int QPT = NQW + XQ;                                 // quarters per K-tile
   // prologue: K-tile 0 whole, the first half of K-tile 1's quarters
@@ -372,6 +403,9 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
     }
     barrier_lds();
     if (kt == nk - 1) {
+      const bool more = t + 1 < G && !(DBG & 2);
+      Side nxt;
+      if (more) nxt = side_fetch(s1);                           // in flight under the epilogue
       if constexpr ((DBG & 1) != 0) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
@@ -382,9 +416,9 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
         epilogue(s0);
       }
       zero();
-      if (t + 1 < G && !(DBG & 2)) {
+      if (more) {
         __syncthreads();                                        // every epilogue done with the side data
-        load_side(s1);
+        side_store(nxt);
         __syncthreads();
       }
     }
@@ -413,15 +447,15 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
   }
 #ifdef XS8_ABLATE
   if constexpr (EPI == EPI_RESID) {   // K-loop / epilogue split of the fp8 FFN down (no epilogue; no MFMA; neither)
-    switch (a.dbg & 15) {
+    // MXDBG = 256 x (kernel DBG bits): 1 no epilogue, 2 side data for the first tile only, 4 no MFMA, 8 no LDS fragment reads, 16 no DMA, 64 E = QPT / 2
+#define TONE_MXA(d) \
+  case d: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, d, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+    switch (a.dbg >> 8) {
       case 0: break;
-      case 1: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 1, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 4: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 4, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 5: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 5, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 8: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 64, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
-      case 9: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 65, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
+      TONE_MXA(1) TONE_MXA(3) TONE_MXA(4) TONE_MXA(5) TONE_MXA(13) TONE_MXA(21) TONE_MXA(29) TONE_MXA(31) TONE_MXA(64) TONE_MXA(65)
       default: return hipErrorInvalidValue;
     }
+#undef TONE_MXA
   }
 #endif
   if (a.rs_inv) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
@@ -726,7 +760,8 @@ hipError_t gemm_mx(const MxArgs& a0, int epi, hipStream_t st) {
   a.prio = knobs().prio_mx;
   // 128 W rows per tile: the 256-row tile needs 96 fragment VGPRs per wave at 32 bytes per lane and
   // spills at two waves per SIMD
-  if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || (a.ldc % 8) || a.N % 128) return hipErrorInvalidValue;
+  if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || a.ldas % 4 || (a.ldc % 8) || a.N % 128)
+    return hipErrorInvalidValue;
   switch (epi) {
     case EPI_SWIGLU: return (!a.C8 || !a.C8s) ? hipErrorInvalidValue : launch_mx<128, EPI_SWIGLU>(a, st);
     // 128 X rows per tile while there are few 256-row tiles (FFN down at M = 10240: 22.0 vs 31.7 us, M = 2560-5120:
