@@ -497,8 +497,29 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   const int q = (items + 7) >> 3, ibeg = xcd * q, iend = min(items, ibeg + q);
   if (ibeg + jb >= iend) return;                                  // workgroup-uniform
 
-  for (int i = tid; i < p.N * (kX8K / 32); i += 512) sWs[i] = p.Ws[i];
-  for (int i = tid; i < p.N; i += 512) sb[i] = p.bias ? p.bias[i] : 0.f;
+  // W scales and bias for the launch: 16-byte pieces, every load ahead of the LDS stores (a byte-wise
+  // load/store loop here was 72 dependent round trips per thread at N = 3072)
+  if ((((uintptr_t)p.Ws | (uintptr_t)p.bias) & 15) == 0) {
+    constexpr int kSq = (kX8MaxN * (kX8K / 32) / 16 + 511) / 512, kBq = (kX8MaxN / 4 + 511) / 512;
+    const int nsq = p.N * (kX8K / 32) / 16, nbq = p.N / 4;
+    u32x4 vs[kSq];
+    f32x4 vb[kBq];
+#pragma unroll
+    for (int q = 0; q < kSq; ++q)
+      if (tid + 512 * q < nsq) vs[q] = reinterpret_cast<const u32x4*>(p.Ws)[tid + 512 * q];
+#pragma unroll
+    for (int q = 0; q < kSq; ++q)
+      if (tid + 512 * q < nsq) reinterpret_cast<u32x4*>(sWs)[tid + 512 * q] = vs[q];
+#pragma unroll
+    for (int q = 0; q < kBq; ++q)
+      if (tid + 512 * q < nbq) vb[q] = p.bias ? reinterpret_cast<const f32x4*>(p.bias)[tid + 512 * q] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < kBq; ++q)
+      if (tid + 512 * q < nbq) reinterpret_cast<f32x4*>(sb)[tid + 512 * q] = vb[q];
+  } else {
+    for (int i = tid; i < p.N * (kX8K / 32); i += 512) sWs[i] = p.Ws[i];
+    for (int i = tid; i < p.N; i += 512) sb[i] = p.bias ? p.bias[i] : 0.f;
+  }
   __syncthreads();                                                // no DMA in flight yet
 
   auto dma = [&](int t) {
