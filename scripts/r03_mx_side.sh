@@ -2,7 +2,7 @@
 # positions); then the fp8 GPU tests
 set -u
 mkdir -p gpurun_out
-O=gpurun_out/r03_mx_side.jsonl
+O=gpurun_out/${OUT:-r03_mx_side}.jsonl
 : > $O
 for r in 1 2; do
   for b in gemm_bench_old gemm_bench; do
@@ -14,6 +14,6 @@ for r in 1 2; do
     echo "$b down M=5120" >> $O; timeout -k 5 90 t-one_amd/$b 5120 1536 384 1 99 1 50 >> $O 2>&1 || exit $?
   done
 done
-CODES="1 3 29 31" ROUNDS=1 OUT=r03_mx_resid_ablate4 bash scripts/r03_mx_resid_ablate2.sh || exit $?
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "fp8" > gpurun_out/r03_mx_side_tests.log 2>&1
+CODES="1 3 29 31" ROUNDS=1 OUT=${OUT:-r03_mx_side}_ablate bash scripts/r03_mx_resid_ablate2.sh || exit $?
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "fp8" > gpurun_out/${OUT:-r03_mx_side}_tests.log 2>&1
 echo "tests rc=$?"

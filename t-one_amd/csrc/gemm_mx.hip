@@ -326,8 +326,6 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   Pos s2 = s1;
   advance(s2);
   zero();
-  side_store(side_fetch(s0));
-  __syncthreads();                                              // side data visible; no DMA in flight yet
   constexpr int QPT = NQW + XQ;                                 // quarters per K-tile
   // prologue: K-tile 0 whole, the first half of K-tile 1's quarters
   // E quarters of K-step t + 2 go out after the stage-freeing barrier of step t, the other QPT - E in the first
@@ -336,8 +334,11 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   // restores E = QPT / 2 for the A/B
   constexpr int E = (DBG & 64) ? QPT / 2 : QPT;
   issue_kt(0, s0, 0, QPT);
+  if (G > 1) issue_kt(1, s1, 0, E);
+  // the first tile's side data behind the prologue DMA (its latency overlaps the ring fill; the region is disjoint)
+  side_store(side_fetch(s0));
+  __syncthreads();                                              // side data visible
   if (G > 1) {
-    issue_kt(1, s1, 0, E);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * E) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
