@@ -435,6 +435,9 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
   int grid = 256;
   const int need = ((ntiles + 7) / 8) * 8;
   if (grid > need) grid = need;
+#ifdef XS8_ABLATE
+  if (getenv("MXGRID")) grid = std::min(grid, atoi(getenv("MXGRID")));   // persistent-grid size sweep
+#endif
   if constexpr (EPI == EPI_SWIGLU) {   // microbenchmark ablations (tools/gemm_bench MXDBG)
     switch (a.dbg) {
       case 0: break;
