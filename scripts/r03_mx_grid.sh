@@ -11,3 +11,12 @@ for r in 1 2; do
   done
 done
 echo done
+# one barrier per K-step instead of two (DBG 128 drops the mid-step one; races, so timing only)
+O2=gpurun_out/r03_mx_barrier.jsonl
+: > $O2
+for r in 1 2; do
+  for c in 1 129 31 159; do
+    echo "down DBG=$c" >> $O2; MXDBG=$((256 * c)) timeout -k 5 90 t-one_amd/gemm_bench_ablate 40960 1536 384 1 99 1 50 >> $O2 2>&1 || exit $?
+  done
+done
+echo done2

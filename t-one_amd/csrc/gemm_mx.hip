@@ -379,7 +379,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
       for (int j = 2; j < 4; ++j)
         acc[i][j] = (DBG & 4) ? acc[i][j] + (float)(wa[i][2] ^ xf[j][3] ^ wsa[i] ^ xs[j])
                               : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[i], xf[j], acc[i][j], 0, 0, 0, wsa[i], 0, xs[j]);
-    barrier_lds();                                              // every wave's reads of stage buf done
+    if constexpr (!(DBG & 128)) barrier_lds();                  // every wave's reads of stage buf done (128: timing only)
     // phase 2
     if (t + 2 < G) issue_kt(t + 2, s2, 0, (E + 1) / 2);
 #pragma unroll
@@ -451,12 +451,12 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
   }
 #ifdef XS8_ABLATE
   if constexpr (EPI == EPI_RESID) {   // K-loop / epilogue split of the fp8 FFN down (no epilogue; no MFMA; neither)
-    // MXDBG = 256 x (kernel DBG bits): 1 no epilogue, 2 side data for the first tile only, 4 no MFMA, 8 no LDS fragment reads, 16 no DMA, 64 E = QPT / 2
+    // MXDBG = 256 x (kernel DBG bits): 1 no epilogue, 2 side data for the first tile only, 4 no MFMA, 8 no LDS fragment reads, 16 no DMA, 64 E = QPT / 2, 128 no mid-step barrier (races: timing only)
 #define TONE_MXA(d) \
   case d: hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, d, BMX>), dim3(grid), dim3(512), 0, st, a); return hipGetLastError();
     switch (a.dbg >> 8) {
       case 0: break;
-      TONE_MXA(1) TONE_MXA(3) TONE_MXA(4) TONE_MXA(5) TONE_MXA(13) TONE_MXA(21) TONE_MXA(29) TONE_MXA(31) TONE_MXA(64) TONE_MXA(65)
+      TONE_MXA(1) TONE_MXA(3) TONE_MXA(4) TONE_MXA(5) TONE_MXA(13) TONE_MXA(21) TONE_MXA(29) TONE_MXA(31) TONE_MXA(64) TONE_MXA(65) TONE_MXA(129) TONE_MXA(159)
       default: return hipErrorInvalidValue;
     }
 #undef TONE_MXA
