@@ -105,35 +105,46 @@ def family_weight_bytes(precision: str = "fp32") -> dict:
             "gemm_sub_out": C.SUB_OUT_IN * d * ew, "gemm_reduce": 4 * d * d * ew}
 
 
+# launches per 300 ms step of each family (session.hip enqueue_step): two FFNs per layer, q/k/v as one launch
+# in layers 0..13 and two (q; k|v) in 14/15
+FAMILY_LAUNCHES = {"gemm_ffn_up": 2 * C.N_LAYERS, "gemm_ffn_down": 2 * C.N_LAYERS,
+                   "gemm_qkv": C.MHSA_STATELESS + 2 * (C.N_LAYERS - C.MHSA_STATELESS),
+                   "gemm_attn_out": C.N_LAYERS, "gemm_pw1": C.N_LAYERS, "gemm_pw2": C.N_LAYERS,
+                   "gemm_sub_out": 1, "gemm_reduce": 1}
+# the residual-output (EPI_RESID) GEMMs: one kernel family in the traffic summary, the HBM-bound one
+RESID_FAMILIES = ("gemm_ffn_down", "gemm_attn_out", "gemm_pw2")
+
+
 def measured_traffic(family: str, precision: str, batch: int):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (scripts/pmc_traffic.sh + scripts/traffic_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950
-    correction), or (None, None) when no summary exists for this precision / batch."""
-    for rnd in ("r03", "r02", "r01"):   # the newest round's summary first
+    """HBM bytes per launch of a GEMM family ("gemm_ffn_up", or "resid" = every EPI_RESID launch) from the
+    committed rocprofv3 PMC summary (scripts/pmc_traffic.sh + scripts/traffic_summary.py: FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950 correction), or (None, None) when no summary covers this precision / batch / family."""
+    for rnd in ("r04", "r03", "r02", "r01"):   # the newest round's summary first
         path = os.path.join(ROOT, "profiles", f"{rnd}_traffic_{precision}_b{batch}.json")
         try:
             with open(path) as fh:
                 t = json.load(fh)
-            break
         except (OSError, ValueError):
             continue
-    else:
-        return None, None
-    if t.get("kernel") != family:
-        return None, None
-    return int(t["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+        fam = t.get("families", {}).get(family)
+        if fam is None and t.get("kernel") == family:
+            fam = t
+        if fam is None:
+            continue
+        return int(fam["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
-def algo_bytes(family: str, precision: str, batch: int) -> float:
-    """Algorithmic HBM bytes per launch of a GEMM family: A read + W read + C write, averaged over the
-    family's launches in one step (only the FFN up-projection is modelled)."""
-    if family != "gemm_ffn_up":
-        return 0.0
-    e = 2 if precision == "bf16" else 4
-    d, ff = C.D_MODEL, C.D_FF
-    per = [e * (batch * C.layer_frames(l) * d + 2 * ff * d + batch * C.layer_frames(l) * ff)
-           for l in range(C.N_LAYERS) for _ in range(2)]
-    return sum(per) / len(per)
+def algo_bytes(family: str, precision: str, batch: int, T: int = C.CHUNK_FRAMES) -> float:
+    """Algorithmic HBM bytes per launch of a GEMM family, averaged over the family's launches in one step:
+    activations in and out at the precision's element sizes (family_bytes_per_stream: fp8 operands at
+    1 + 1/32 B per element, bf16 at 2, fp32 at 4; residual in/out fp32 + bf16 shadow for RESID outputs) x
+    batch, plus the weights every launch reads once.  family "resid" = the three EPI_RESID families together
+    (FFN down, attn-out, pw2), the unit the PMC summary measures."""
+    pb, wb = family_bytes_per_stream(T, precision), family_weight_bytes(precision)
+    fams = RESID_FAMILIES if family == "resid" else (family,)
+    tot = sum(pb[f] * batch + wb[f] for f in fams)
+    return tot / sum(FAMILY_LAUNCHES[f] for f in fams)
 
 
 def synthetic_pcm(rng, b, n_chunks, silence=0.2, chunk=C.AUDIO_CHUNK_SAMPLES):
@@ -296,9 +307,27 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
             floor_sum += fl
             fam_roof[k] = {"us_per_step": round(us, 1), "bound": bnd, "floor_us": round(fl, 1),
                            "frac": round(fl / us, 3), "gb_per_step": round((pb[k] * B + wb[k]) / 1e9, 4)}
+        # the HBM-bound residual-output family (FFN down, attn-out, pw2: every EPI_RESID launch), priced on
+        # HBM: algorithmic bytes per launch / mean launch time vs 8 TB/s, and its PMC traffic per launch
+        resid = None
+        rf = [k for k in RESID_FAMILIES if k in fams]
+        if rf:
+            r_launch = sum(fams[k]["launches_per_step"] for k in rf)
+            r_us = sum(fams[k]["avg_us"] * fams[k]["launches_per_step"] for k in rf) / r_launch
+            r_bytes = algo_bytes("resid", precision, B, fr)
+            r_traffic, r_src = measured_traffic("resid", precision, B) if chunk == 2400 else (None, None)
+            resid = {"bound": "hbm", "kernels": "EPI_RESID launches (FFN down, attn-out, pw2)",
+                     "launches_per_step": r_launch, "avg_us": round(r_us, 2), "algo_bytes": int(r_bytes),
+                     "achieved": round(r_bytes / (r_us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(r_bytes / (r_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), "traffic": r_traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": r_src,
+                     "traffic_over_algo": round(r_traffic / r_bytes, 3) if r_traffic else None}
+        a_bytes = algo_bytes(dom, precision, B, fr)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": tsrc, "algo_bytes": int(algo_bytes(dom, precision, B)) if chunk == 2400 else None,
+                "traffic_source": tsrc, "algo_bytes": int(a_bytes),
+                "traffic_over_algo": round(traffic / a_bytes, 3) if traffic else None,
+                "resid_family": resid,
                 "avg_us": round(f["avg_us"], 2), "flop_per_launch": int(f["flop_per_launch"]),
                 "step_tflops": round(C.FLOP_PER_CHUNK * B / (elapsed / args.steps) / 1e12, 2) if chunk == 2400 else None,
                 "encoder_gemm_tflops": round(gemm_flop / (gemm_us * 1e-6) / 1e12, 2),

@@ -1,29 +1,40 @@
-"""Per-launch HBM traffic of the FFN up-projection launches from the PMC passes of
-scripts/pmc_traffic.sh.  FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the
-bytes of wide streaming reads (MI355X_MICROARCH.md, HBM), so fetch bytes = 2 x FETCH_SIZE x 1024.
-The FFN up-projection is the only GEMM with the SWIGLU epilogue; its kernels are recognised by name.
+"""Per-launch HBM traffic of two GEMM families from the PMC passes of scripts/pmc_traffic.sh: the FFN
+up-projection (the only SWIGLU GEMM) and the residual-output GEMMs (every EPI_RESID launch: FFN down,
+attn-out, pw2), recognised by kernel name and epilogue template argument.  FETCH_SIZE / WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM), so
+fetch bytes = 2 x FETCH_SIZE x 1024.
 Usage: python scripts/traffic_summary.py gpurun_out/pmc_<prec> <prec> <batch> > profiles/<file>.json"""
 import csv, glob, json, re, sys
 
 root, prec, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
-PAT = {  # SWIGLU instantiations: EPI_SWIGLU = 2
-    "fp32": re.compile(r"gemm_x3_kernel<.*XT<\d+, \d+, \d+, \d+, \d+, \d+>, 2, (true|false), (true|false)(, (true|false))*>"),
-    "fp32-mfma": re.compile(r"gemm_kernel<tone::Tile<\d+, \d+, \d+, \d+>, 2,"),
-    "bf16": re.compile(r"(gemm_t_kernel<.*TT<\d+, \d+, \d+, \d+>, 2, (true|false)>|gemm_xs_kernel<2, )"),
-    "fp8": re.compile(r"(gemm_xs8_kernel<2, |gemm_mx_kernel<\d+, 2, )"),
+UP = {  # SWIGLU instantiations: EPI_SWIGLU = 2
+    "fp32": r"gemm_x3_kernel<tone::XT<[^>]*>, 2,",
+    "fp32-mfma": r"gemm_kernel<tone::Tile<[^>]*>, 2,",
+    "bf16": r"(gemm_t_kernel<tone::TT<[^>]*>, 2,|gemm_xs\d?_kernel<2, )",
+    "fp8": r"(gemm_xs8_kernel<2, |gemm_mx_kernel<\d+, 2, )",
 }[prec]
+# EPI_RESID = 1, in any GEMM kernel family
+RESID = (r"(gemm_x3_kernel<tone::XT<[^>]*>, 1,|gemm_glds_kernel<tone::Tile<[^>]*>, 1,|gemm_kernel<tone::Tile<[^>]*>, 1,"
+         r"|gemm_t_kernel<tone::TT<[^>]*>, 1,|gemm_f32t_kernel<[^>]*>, 1,|gemm_mx_kernel<\d+, 1,)")
 
 
-def per_launch(sub):
+def per_launch(sub, pat):
     f = glob.glob(f"{root}/{sub}/**/*counter_collection.csv", recursive=True)[0]
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if PAT.search(r["Kernel_Name"])]
-    return vals
+    return [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if re.search(pat, r["Kernel_Name"])]
 
 
-fetch, write = per_launch("fetch"), per_launch("write")
-fb = 2 * 1024 * sum(fetch) / len(fetch)
-wb = 1024 * sum(write) / len(write)
-print(json.dumps({"kernel": "gemm_ffn_up", "precision": prec, "batch": batch, "launches_fetch": len(fetch),
-                  "launches_write": len(write), "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
-                  "traffic_bytes_per_launch": round(fb + wb),
-                  "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes, eager launches; fetch x2 (gfx950)"}))
+def family(pat):
+    fetch, write = per_launch("fetch", pat), per_launch("write", pat)
+    if not fetch or not write:
+        return None
+    fb = 2 * 1024 * sum(fetch) / len(fetch)
+    wb = 1024 * sum(write) / len(write)
+    return {"launches_fetch": len(fetch), "launches_write": len(write), "fetch_bytes_per_launch": round(fb),
+            "write_bytes_per_launch": round(wb), "traffic_bytes_per_launch": round(fb + wb)}
+
+
+up, resid = family(UP), family(RESID)
+out = {"kernel": "gemm_ffn_up", "precision": prec, "batch": batch, **(up or {}),
+       "families": {k: v for k, v in (("gemm_ffn_up", up), ("resid", resid)) if v},
+       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes, eager launches; fetch x2 (gfx950)"}
+print(json.dumps(out))

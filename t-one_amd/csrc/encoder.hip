@@ -374,13 +374,9 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g,
 template <int T, bool OBF>
 static hipError_t launch_dwconv_t(const void* g, StateRef s, int layer, const float* w, const float* b, void* out,
                                   int B, hipStream_t st) {
-  const int forced = knobs().dwconv_variant;   // TONE_DWCONV_VARIANT (sweeps only): 0 = 384x2, 1 = 128x1, 2 = 384x1, 3 = 192x1
-  const int v = forced >= 0 ? forced : (B >= 1024 ? 3 : 1);   // profiles/r01_dwconv_sweep.txt
-  if (v == 0)
-    hipLaunchKernelGGL((dwconv_kernel<T, OBF, kD, 2>), dim3((B + 1) / 2, 1), dim3(kD), 0, st, g, s, layer, w, b, out, B);
-  else if (v == 2)
-    hipLaunchKernelGGL((dwconv_kernel<T, OBF, kD, 1>), dim3(B, 1), dim3(kD), 0, st, g, s, layer, w, b, out, B);
-  else if (v == 3)
+  // block shape by batch: 192 channels x 1 stream from B = 1024, else 128 x 1 (profiles/r01_dwconv_sweep.txt,
+  // r03_dwconv_sweep.txt)
+  if (B >= 1024)
     hipLaunchKernelGGL((dwconv_kernel<T, OBF, 192, 1>), dim3(B, 2), dim3(192), 0, st, g, s, layer, w, b, out, B);
   else
     hipLaunchKernelGGL((dwconv_kernel<T, OBF, 128, 1>), dim3(B, kD / 128), dim3(128), 0, st, g, s, layer, w, b, out, B);

@@ -461,7 +461,7 @@ __host__ __device__ __forceinline__ int p3_swz(int row) {   // 16-byte chunk XOR
 template <int T>
 __global__ void __launch_bounds__(512) conv2_p3_kernel(const float* __restrict__ x2, const uint16_t* __restrict__ w2p,
                                                      const float* __restrict__ scale, const float* __restrict__ shift,
-                                                     float* __restrict__ flat, int prio) {
+                                                     float* __restrict__ flat) {
   constexpr int NWV = 8;
   constexpr int kParts = (T + kP3Rows - 1) / kP3Rows;
   constexpr int kIn = (T == make_geom(3200).T ? make_geom(3200) : make_geom(2400)).sub2In;   // input rows per stream
@@ -479,8 +479,6 @@ __global__ void __launch_bounds__(512) conv2_p3_kernel(const float* __restrict__
   float* sh = sc + kSub2C;
   const int b = blockIdx.x / kParts, part = blockIdx.x % kParts;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // static priority (A/B, TONE_C2_PRIO): 1 = the row-staging waves 4-7, 2 = the W-ring waves 0-3
-  if ((prio == 1 && wid >= 4) || (prio == 2 && wid < 4)) __builtin_amdgcn_s_setprio(1);
   const int rows = min(kP3Rows, T - part * kP3Rows), posT = rows * kSub2F;
   const float* xb = x2 + (int64_t)b * kIn * kSub1F * kSub1C;
   if (tid < kSub2C) {
@@ -638,9 +636,8 @@ hipError_t launch_conv2_p3(const void* x2, const void* w2p, const float* scale, 
   const float* xs = static_cast<const float*>(x2);
   const uint16_t* ws = static_cast<const uint16_t*>(w2p);
   float* fl = static_cast<float*>(flat);
-  const int prio = knobs().c2_prio;
-  if (T == 13) hipLaunchKernelGGL((conv2_p3_kernel<13>), dim3(3 * B), dim3(512), 0, st, xs, ws, scale, shift, fl, prio);
-  else if (T == kT) hipLaunchKernelGGL((conv2_p3_kernel<kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl, prio);
+  if (T == 13) hipLaunchKernelGGL((conv2_p3_kernel<13>), dim3(3 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
+  else if (T == kT) hipLaunchKernelGGL((conv2_p3_kernel<kT>), dim3(2 * B), dim3(512), 0, st, xs, ws, scale, shift, fl);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -509,7 +509,6 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
   float* rden = reinterpret_cast<float*>(lds + S * kStageElems);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (p.prio && __builtin_amdgcn_readfirstlane(wid) >= TL::WM * TL::WN / 2) __builtin_amdgcn_s_setprio(1);
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = p.N / BN;
   int bm, bn;
@@ -887,9 +886,7 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   const int bk = bf16 ? 64 : 32;
   if (bf16 && a.a_bf16) {
     if (a.K % 64 != 0 || a.N % 128 != 0 || a.M <= 0 || (epi == EPI_RESID && a.c_bf16)) return hipErrorInvalidValue;
-    GemmArgs b = a;
-    b.prio = knobs().prio_bf16;
-    return gemm_bf16(b, epi, st);
+    return gemm_bf16(a, epi, st);
   }
   if (!bf16 && a.W3 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
     // fp32 by exact bf16 splitting (gemm_t.hip gemm_x3); tile per shape from tools/gemm_bench

@@ -134,7 +134,6 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   float* sb = reinterpret_cast<float*>(sX + BMX * kMxKB);
   float* sr = sb + BNW;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (p.prio && wid >= 4) __builtin_amdgcn_s_setprio(1);   // static priority, second half (gemm_mx() sets prio)
   const int wn = wid / WMW, wm = wid % WMW, l15 = lane & 15, lg = lane >> 4, g = mx_swz(l15);
   const int ntn = p.N / BNW, ntm = (p.M + BMX - 1) / BMX, ntiles = ntn * ntm;
   const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
@@ -437,7 +436,6 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
   if (grid > need) grid = need;
 #ifdef XS8_ABLATE
   if (getenv("MXGRID")) grid = std::min(grid, atoi(getenv("MXGRID")));   // persistent-grid size sweep
-#endif
   if constexpr (EPI == EPI_SWIGLU) {   // microbenchmark ablations (tools/gemm_bench MXDBG)
     switch (a.dbg) {
       case 0: break;
@@ -449,7 +447,6 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
       default: return hipErrorInvalidValue;
     }
   }
-#ifdef XS8_ABLATE
   if constexpr (EPI == EPI_RESID) {   // K-loop / epilogue split of the fp8 FFN down (no epilogue; no MFMA; neither)
     // MXDBG = 256 x (kernel DBG bits): 1 no epilogue, 2 side data for the first tile only, 4 no MFMA, 8 no LDS fragment reads, 16 no DMA, 64 E = QPT / 2, 128 no mid-step barrier (races: timing only)
 #define TONE_MXA(d) \
@@ -781,8 +778,7 @@ hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st) {
 }
 
 hipError_t gemm_mx(const MxArgs& a0, int epi, hipStream_t st) {
-  MxArgs a = a0;
-  a.prio = knobs().prio_mx;
+  const MxArgs& a = a0;
   // 128 W rows per tile: the 256-row tile needs 96 fragment VGPRs per wave at 32 bytes per lane and
   // spills at two waves per SIMD
   if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || a.ldas % 4 || (a.ldc % 8) || a.N % 128)

@@ -48,7 +48,6 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_t_kernel(GemmArgs p
   float* sbias = rden + 2 * BMX;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (p.prio && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);   // static priority, second half (gemm() sets prio)
   const int wn = wid / WM, wm = wid % WM;
   const int lr = lane & 31, lh = lane >> 5, cs = (lr >> 1) & 7;
   const int ntn = p.N / BNW, ntm = (p.M + BMX - 1) / BMX, ntiles = ntn * ntm;
@@ -526,15 +525,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   const int lr = lane & 31, lh = lane >> 5;
   const int ntn = p.N / BNW;
   int m0, n0;
-  if (p.xcd_a) {
-    // 2D XCD blocks: XCD x owns n-tiles of group x % a and m-tiles of group x / a, so its compulsory L2
-    // fill is W / a + X / (8 / a) instead of all of W (or all of X); the launcher picks a and checks
-    // the divisibility (grid = tiles, a multiple of 8)
-    const int a = p.xcd_a, xcd = blockIdx.x & 7, li = blockIdx.x >> 3;
-    const int npg = ntn / a, mpg = ((p.M + BMX - 1) / BMX) / (8 / a);
-    n0 = ((xcd % a) * npg + li % npg) * BNW;
-    m0 = ((xcd / a) * mpg + li / npg) * BMX;
-  } else if ((ntn & 7) == 0) {
+  if ((ntn & 7) == 0) {
     // large W (FFN up: 7 MB of planes > one XCD's 4 MB L2): XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8)
     // for every M-tile, so each W plane row is fetched into one L2 only and the X tile is reused
     // by the XCD's N-tiles back to back
@@ -746,31 +737,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
 }
 
-// XCD blocking for gemm_x3 (GemmArgs::xcd_a): the a in {1, 2, 4, 8} whose per-XCD compulsory fill
-// (W planes / a + X / (8 / a)) is smallest, or 0 (default order) when the tiles do not divide evenly.
-// Off unless TONE_X3_XCD=1: on FFN up at B = 256 it raises the L2 hit rate from 0.81 to 0.87 and halves
-// the fabric fetch (30 -> 18 MB) without changing the time (49.8 vs 49.2 us) -- the kernel is bound by
-// its LDS-DMA issue rate, not by L2 misses.
-template <class TL>
-int x3_xcd_split(const GemmArgs& a) {
-  const bool off = !knobs().x3_xcd;
-  const int ntn = a.N / TL::BNW, ntm = (a.M + TL::BMX - 1) / TL::BMX;
-  if (off || a.k_split || (ntn & 7) == 0 || a.M % TL::BMX) return 0;
-  const double wb = 6.0 * a.N * a.K, xb = (a.a_plane ? 6.0 : 4.0) * a.M * a.K;
-  int best = 0;
-  double cost = wb + xb / 8;                      // the default XCD-contiguous m-major order: all of W
-  for (int s = 2; s <= 8; s *= 2) {
-    if (ntn % s || ntm % (8 / s)) continue;
-    const double c = wb / s + xb / (8 / s);
-    if (c < 0.8 * cost) { cost = c; best = s; }
-  }
-  return best;
-}
-
 template <class TL, int EPI>
 hipError_t launch_x3(const GemmArgs& a0, hipStream_t st) {
   GemmArgs a = a0;
-  a.xcd_a = x3_xcd_split<TL>(a0);
   // static priority for waves NW/2.. (default; TONE_X3_PRIO=0 turns it off): fp32 B = 256 step 3.616 -> 3.583 ms,
   // FFN down 897 -> 871 us (profiles/r02_ab_x3_prio.jsonl)
   if (knobs().x3_prio) a.dbg |= 64;

@@ -4,18 +4,17 @@
 // Why: with K = 384 a 256 x 256 output tile does only 2 * 256 * 256 * 384 FLOP per (256 + 256) x 384 x 2 bytes
 // staged through LDS (128 FLOP/B), and gemm_t's loop is bound by that LDS-DMA fill (~32 GB/s per CU) plus a
 // SwiGLU epilogue during which every wave of the CU idles the matrix pipe.  Here
-//   * one wave per SIMD (4 per workgroup, 512 registers each); each wave keeps ITS OWN 64 X rows x 384 K in
-//     registers for a whole work item (192 VGPRs of bf16 fragments, loaded once from L2 / HBM, with the
-//     folded-RMSNorm row sums taken from them), so only W
-//     streams through LDS: 64 W rows x 384 K (48 KiB) per tile for 2 x 64 x 256 x 384 FLOP = 262 FLOP/B,
-//     twice gemm_t's;
+//   * eight waves, two per SIMD (256 registers each); each wave keeps ITS OWN 32 X rows x 384 K in registers
+//     for a whole work item (96 VGPRs of bf16 fragments, kXsMB = 2 m-blocks of 16 rows, loaded once from L2 /
+//     HBM, with the folded-RMSNorm row sums taken from them), so only W streams through LDS: 64 W rows x 384 K
+//     (48 KiB) per tile for 2 x 64 x 256 x 384 FLOP = 262 FLOP/B per workgroup (256 X rows), twice gemm_t's;
 //   * the W tiles go through a 3-deep LDS ring by global_load_lds_dwordx4, tile t + 2 issued as soon as tile t
 //     starts (its slot held tile t - 1, whose reads every wave finished before the barrier), so a tile has two
 //     tiles of MFMAs to land; every lane issues a fixed number of stores per tile, which keeps the counted
 //     vmcnt exact;
 //     16-byte chunk c of W row r sits at LDS slot c ^ (r & 15) of its 768-byte row, which makes every
 //     ds_read_b128 of the 16x16x32 fragment map conflict-free;
-//   * the accumulators are small (4 m-blocks x 4 n-blocks x 4 per lane), so they are double-buffered: the
+//   * the accumulators are small (2 m-blocks x 4 n-blocks x 4 per lane), so they are double-buffered: the
 //     epilogue of tile t - 1 (bias, SwiGLU / GLU, bf16 pack, stores) is interleaved with the MFMAs of tile
 //     t in the same wave instead of running with the matrix pipe idle.
 // Work item = (256 X rows, a run of nc W tiles); items are dealt so the items of one X row block share an
@@ -40,7 +39,7 @@ constexpr int kXsBN = 64;                 // W rows per tile
 constexpr int kXsRowB = kXsK * 2;         // bytes per W row (768)
 constexpr int kXsTile = kXsBN * kXsRowB;  // 48 KiB
 constexpr int kXsR = 3;                   // W ring depth
-constexpr int kXsPieces = kXsTile / 1024 / kXsWaves;   // 1 KiB DMA pieces per wave per tile (12)
+constexpr int kXsPieces = kXsTile / 1024 / kXsWaves;   // 1 KiB DMA pieces per wave per tile (6)
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t2 __attribute__((ext_vector_type(4)));
@@ -97,7 +96,7 @@ __global__ void __launch_bounds__(kXsWaves * 64) gemm_xs_kernel(GemmArgs p, int 
   for (int item = ibeg + jb; item < iend; item += nxb) {
     const int mt = item / nch, ch = item % nch;
     const int t0 = ch * nc, t1 = min(nwt, t0 + nc), n = t1 - t0;
-    const int mbase = mt * kXsBM + wid * 16 * kXsMB;              // this wave's 64 X rows
+    const int mbase = mt * kXsBM + wid * 16 * kXsMB;              // this wave's 32 X rows
 
     // this wave's X fragments: m-block mb, K-step ks -> lane holds row mbase + 16 mb + l15, k 32 ks + 8 lg ..
     bf16x8_t xf[kXsMB][kXsKS];

@@ -12,13 +12,8 @@ namespace tone {
 // Experiment switches, read from the environment ONCE per process (the first call; A/B runs compare separate
 // processes).  Defaults are the measured best; none of them changes the arithmetic.
 struct Knobs {
-  int prio_bf16;       // TONE_PRIO_BF16=1: static priority for waves 4-7 in the bf16 LDS-DMA GEMMs (default off)
-  int prio_mx;         // TONE_PRIO_MX=1: the same in the MXFP8 GEMMs (default off)
   int x3_prio;         // TONE_X3_PRIO=0: no static priority in gemm_x3 (default on)
-  int x3_xcd;          // TONE_X3_XCD=1: 2D XCD tile blocks in gemm_x3 (default off)
   int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand
-  int dwconv_variant;  // TONE_DWCONV_VARIANT: force a dwconv block shape (-1 = by batch)
-  int c2_prio;         // TONE_C2_PRIO: static priority role in conv2_p3 (default 0)
 };
 const Knobs& knobs();
 
@@ -58,9 +53,6 @@ struct GemmArgs {
   int64_t c_plane;    // STORE / SWIGLU / GLU: C written as 3 bf16 planes instead of fp32
   int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
   int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
-  int prio;           // bf16 kernels: static priority for the second half of the waves (set by gemm(), TONE_PRIO_BF16)
-  int xcd_a;          // gemm_x3: XCD x owns the 2D tile block (n-group x % a, m-group x / a) of an a x (8 / a)
-                      // split (set by the launcher; 0 = the default order)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -102,7 +94,6 @@ struct MxArgs {
   int64_t ldc8s;
   int M, N, K;
   int dbg;                // microbenchmarks only (gemm_mx.hip DBG bits); 0 in the session
-  int prio;               // static priority for waves 4-7 (set by gemm_mx(), TONE_PRIO_MX)
 };
 hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st);
 // X-stationary MXFP8 GEMM for K = 384 (gemm_mx.hip gemm_xs8_kernel): SWIGLU (-> MXFP8 h) / STORE (bf16 out)

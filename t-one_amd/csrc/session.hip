@@ -31,13 +31,8 @@ const Knobs& knobs() {
       return e && *e ? std::atoi(e) : dflt;
     };
     Knobs r;
-    r.prio_bf16 = env("TONE_PRIO_BF16", 0) == 1;
-    r.prio_mx = env("TONE_PRIO_MX", 0) == 1;
     r.x3_prio = env("TONE_X3_PRIO", 1) != 0;
-    r.x3_xcd = env("TONE_X3_XCD", 0) == 1;
     r.fp8_normq = env("TONE_FP8_NORMQ", 1) != 0;
-    r.dwconv_variant = env("TONE_DWCONV_VARIANT", -1);
-    r.c2_prio = env("TONE_C2_PRIO", 0);
     return r;
   }();
   return k;

@@ -32,3 +32,50 @@ def test_family_bytes_and_bounds():
     assert b["gemm_ffn_up"] == "mfma"
     assert b["gemm_ffn_down"] == b["gemm_attn_out"] == b["gemm_pw2"] == "hbm"
     assert set(bound("fp32", 256).values()) == {"mfma"}
+
+
+def test_algo_bytes_per_launch_by_precision():
+    """The dominant kernel's algorithmic bytes per launch (bench.algo_bytes): the FFN up-projection at
+    B = 4096 reads X and writes h at 2 B per element in bf16 and at 1 + 1/32 B (e4m3 + one E8M0 scale per
+    32) in fp8, plus the 2.36 MB bf16 / 1.22 MB MXFP8 weight matrix; fp32 at 4 B."""
+    d, ff, B = 384, 1536, 4096
+    rows = sum(B * (5 if 6 < l <= 14 else 10) for l in range(16)) * 2 / 32      # mean rows per FFN launch
+    e8 = 1 + 1 / 32
+    want = {"fp32": 4 * rows * (d + ff) + 4 * 2 * ff * d, "bf16": 2 * rows * (d + ff) + 2 * 2 * ff * d,
+            "fp8": e8 * rows * (d + ff) + e8 * 2 * ff * d}
+    for prec, w in want.items():
+        assert abs(bench.algo_bytes("gemm_ffn_up", prec, B) - w) / w < 1e-9, prec
+    assert 61e6 < bench.algo_bytes("gemm_ffn_up", "fp8", B) < 63e6       # VERDICT r3: ~62 MB, not 240.6 MB
+    assert bench.algo_bytes("gemm_ffn_up", "fp8", B) < bench.algo_bytes("gemm_ffn_up", "bf16", B) / 1.9
+
+
+def test_algo_bytes_resid_family():
+    """The EPI_RESID family (FFN down, attn-out, pw2 as one kernel family, 64 launches per step): A read at
+    the operand size, the fp32 residual read and written, the bf16 shadow (bf16 / fp8 modes), W once."""
+    d, ff, B = 384, 1536, 2048
+    tot = 0.0
+    for prec, ea, eh, sh in (("bf16", 2, 2, 2), ("fp8", 2, 1 + 1 / 32, 2), ("fp32", 4, 4, 0)):
+        tot = 0.0
+        for l in range(16):
+            rows = B * (5 if 6 < l <= 14 else 10)
+            tot += 2 * rows * (ff * eh + d * (8 + sh))         # two FFN downs
+            tot += 2 * rows * (d * ea + d * (8 + sh))          # attn-out + pw2
+        ew, e8 = (4, 4) if prec == "fp32" else (2, eh)
+        tot += 16 * (2 * ff * d * e8 + 2 * d * d * ew)
+        got = bench.algo_bytes("resid", prec, B)
+        assert abs(got - tot / 64) / (tot / 64) < 1e-9, prec
+    assert bench.FAMILY_LAUNCHES["gemm_ffn_down"] + bench.FAMILY_LAUNCHES["gemm_attn_out"] + \
+        bench.FAMILY_LAUNCHES["gemm_pw2"] == 64
+
+
+def test_measured_traffic_not_below_algorithmic():
+    """Every committed PMC traffic summary that bench.py quotes must be at least the algorithmic bytes of
+    the launches it measures: a ratio below 1 means the bookkeeping is wrong (VERDICT r3 weak #5)."""
+    import glob, json, os, re
+    for path in sorted(glob.glob(os.path.join(bench.ROOT, "profiles", "r0[34]_traffic_*_b*.json"))):
+        prec, b = re.search(r"traffic_(fp32|bf16|fp8)_b(\d+)\.json", path).groups()
+        t = json.load(open(path))
+        fams = t.get("families") or {"gemm_ffn_up": t}
+        for fam, v in fams.items():
+            ratio = v["traffic_bytes_per_launch"] / bench.algo_bytes(fam, prec, int(b))
+            assert ratio >= 1.0, (path, fam, ratio)

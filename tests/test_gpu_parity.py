@@ -337,8 +337,8 @@ def test_large_batch_staggered_streams(weights, oracle, prec, b, n):
     N = 1 legs of configs 4 / 5 (bf16 / fp8 at B = 4096, the batch bench.py times), 10 stateful 300 ms chunks,
     stream s starting (zero state) at chunk s % 4; 64 sampled streams stepped independently by the oracle
     (its own fp32 state chain, not the device state) and compared every chunk.  These batches route FFN up
-    to the 256 x 256 transposed kernel and the MXFP8 GEMMs to their 256-row X tiles, which the smaller
-    tests do not reach at the same tile counts."""
+    (and, from B = 1536, pw1) to the X-stationary kernels (gemm_xs in bf16, gemm_xs8 in fp8) and the other
+    MXFP8 GEMMs to their 256-row X tiles, which the smaller tests do not reach at the same tile counts."""
     _gpu()
     from tone_amd.model import ToneSession
     pick = np.arange(0, b, b // 64)
