@@ -13,6 +13,7 @@ hipGraph replay, and a slot API over a device-resident state slab.
 from __future__ import annotations
 
 import ctypes
+import logging
 from pathlib import Path
 from typing import Optional
 
@@ -22,6 +23,8 @@ import numpy.typing as npt
 from . import _lib
 from . import config as C
 from .weights import load_weights, synthetic_weights
+
+log = logging.getLogger(__name__)
 
 
 def _torch():
@@ -286,29 +289,43 @@ class StreamingCTCModel:
         return cls.from_local(cls.download_from_hugging_face(), **kw)
 
     @classmethod
-    def download_from_hugging_face(cls) -> str:
+    def download_from_hugging_face(cls, prefer_safetensors: bool = True) -> str:
         """tone/onnx_wrapper.py:52-63 fetches ``model.onnx``.  The torch checkpoint of the same model,
-        ``model.safetensors``, carries every parameter under its own name, so it is tried first; ``model.onnx``
-        (read by :mod:`tone_amd.onnx_weights`, which attributes constant-folded initializers through the graph)
-        is the fallback.  Offline this works when either file is already in the HF cache."""
+        ``model.safetensors``, carries every parameter under its own name and in fp32, so with
+        ``prefer_safetensors`` it is tried first and ``model.onnx`` (read by :mod:`tone_amd.onnx_weights`, which
+        attributes constant-folded initializers through the graph) is the fallback when the repository or the
+        offline cache has no such file.  Any other failure (authentication, network, a corrupt cache) is raised.
+        The file taken is logged."""
         from huggingface_hub import hf_hub_download
-        try:
-            return hf_hub_download(cls.HF_REPO, cls.HF_WEIGHTS)
-        except Exception:      # not published / not cached offline: the reference's own artifact
-            return hf_hub_download(cls.HF_REPO, cls.HF_MODEL)
+        from huggingface_hub.utils import EntryNotFoundError, LocalEntryNotFoundError
+        if prefer_safetensors:
+            try:
+                path = hf_hub_download(cls.HF_REPO, cls.HF_WEIGHTS)
+                log.info("T-one weights: %s", path)
+                return path
+            except (EntryNotFoundError, LocalEntryNotFoundError) as e:
+                log.info("%s/%s not available (%s); using %s", cls.HF_REPO, cls.HF_WEIGHTS, type(e).__name__,
+                         cls.HF_MODEL)
+        path = hf_hub_download(cls.HF_REPO, cls.HF_MODEL)
+        log.info("T-one weights: %s", path)
+        return path
 
     @classmethod
     def from_local(cls, model_path: str | Path, providers: Optional[list[str]] = None, *, device: int = 0,
-                   precision: str = "fp32", max_batch: int = 64) -> "StreamingCTCModel":
+                   precision: str = "fp32", max_batch: int = 64, prefer_safetensors: bool = True) -> "StreamingCTCModel":
         """tone/onnx_wrapper.py:65-78.  ``model_path`` is what the reference passes -- ``model.onnx``
-        (its initializers are read by :mod:`tone_amd.onnx_weights`; a ``model.safetensors`` beside it
-        is preferred when present) -- or a model.safetensors / weights.npz / torch state_dict (.pt,
-        weights_only) / a directory holding one.  ``providers`` is accepted for signature
-        compatibility; the MI355X device is chosen with ``device``."""
+        (its initializers are read by :mod:`tone_amd.onnx_weights`; with ``prefer_safetensors`` a
+        ``model.safetensors`` beside it, the fp32 torch checkpoint of the same model, is taken instead) -- or a
+        model.safetensors / weights.npz / torch state_dict (.pt, weights_only) / a directory holding one.
+        ``providers`` is accepted for signature compatibility; the MI355X device is chosen with ``device``.
+        The file actually loaded is logged."""
         del providers
         p = Path(model_path)
-        if p.suffix == ".onnx" and (p.parent / cls.HF_WEIGHTS).exists():
+        if prefer_safetensors and p.suffix == ".onnx" and (p.parent / cls.HF_WEIGHTS).exists():
+            log.info("T-one weights: %s (found beside %s)", p.parent / cls.HF_WEIGHTS, p.name)
             p = p.parent / cls.HF_WEIGHTS
+        else:
+            log.info("T-one weights: %s", p)
         return cls(ToneSession(load_weights(p), device=device, precision=precision, max_batch=max_batch))
 
     @classmethod

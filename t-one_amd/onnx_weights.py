@@ -30,7 +30,13 @@ autocast, the model wrapped as ``ModelToExport._model``, export.py:144) does not
   parameters; ``Mul`` is an RMSNorm gain;
 * a BatchNorm the exporter fused into its convolution (eval-mode Conv+BatchNormalization peephole) leaves
   no parameters of its own: it is loaded as the identity (gain 1, shift 0, mean 0, var 1 - eps) and the conv
-  carries the fused weight and bias.
+  carries the fused weight and bias -- only when the graph has no BatchNormalization node in that scope and the
+  conv's weight and bias were both attributed through a Conv node.
+
+The node-name convention (``/_model/<module>/<child>/.../<Op>``, nested containers as ``conv.0`` /
+``conv.0.0``) is the one torch.onnx.export's TorchScript exporter writes for scoped modules; it is ASSUMED
+here, not pinned: no export of the reference module is available in this environment (the ``onnx`` package
+is absent, so torch.onnx.export cannot run), and the tests build graphs with the same convention.
 
 Whatever is still unattributed is named in :func:`load_onnx_weights`'s error.
 """
@@ -41,6 +47,8 @@ from pathlib import Path
 from typing import Iterator
 
 import numpy as np
+
+from . import config as C
 
 # TensorProto.DataType -> numpy dtype (raw_data is little-endian)
 _DTYPES = {1: np.float32, 2: np.uint8, 3: np.int8, 4: np.uint16, 5: np.int16, 6: np.int32, 7: np.int64,
@@ -268,6 +276,17 @@ def _roles(node: dict, slot: int, producer_op: str) -> list[str]:
     return []
 
 
+def _bn_conv(bn_scope: str) -> str | None:
+    """The convolution a BatchNorm follows in the T-one module tree: ``pre_encode.conv.<i>.1`` after
+    ``pre_encode.conv.<i>.0`` (conformer_blocks.py:631-641), ``layers.<l>.conv.batch_norm`` after
+    ``layers.<l>.conv.depthwise_conv.conv`` (submodules.py:346-402)."""
+    if bn_scope.endswith(".batch_norm"):
+        return bn_scope[: -len("batch_norm")] + "depthwise_conv.conv"
+    if bn_scope.endswith(".1"):
+        return bn_scope[:-2] + ".0"
+    return None
+
+
 def onnx_state_dict(tensors: dict[str, np.ndarray], nodes: list[dict] | None = None) -> dict[str, np.ndarray]:
     """Map ONNX tensors onto reference parameter names (PARAM_SHAPES), float32 (see the module docstring).
     Missing parameters are left out (:func:`load_onnx_weights` reports them)."""
@@ -303,10 +322,12 @@ def onnx_state_dict(tensors: dict[str, np.ndarray], nodes: list[dict] | None = N
     for nd in nodes:
         for i, x in enumerate(nd["inputs"]):
             consumers.setdefault(x, []).append((nd, i))
-    for name, arr in floats.items():
-        if _strip(name) in PARAM_SHAPES:
-            continue
-        # follow pass-through ops to the first compute node; track transposes
+    via_conv: set[str] = set()            # parameters attributed as a Conv node's weight / bias
+
+    def attribute(name: str, arr: np.ndarray) -> bool:
+        """Walk from one initializer through pass-through ops to the first compute node that names a
+        parameter slot for it; stop at the FIRST successful put (a constant shared by several consumers is
+        written under one key only)."""
         frontier = [(name, False, 0)]
         seen = set()
         while frontier:
@@ -332,28 +353,207 @@ def onnx_state_dict(tensors: dict[str, np.ndarray], nodes: list[dict] | None = N
                 elif nd["op"] == "Gemm" and slot == 1:
                     transposed = tr ^ (not nd["attrs"].get("transB", 0))
                 for role in _roles(nd, slot, ""):
-                    if put(f"{scope}.{role}", arr, transposed):
-                        frontier = []
-                        break
-    # 3) BatchNorm fused into its convolution by the exporter: identity norm
+                    key = f"{scope}.{role}"
+                    if put(key, arr, transposed):
+                        if nd["op"] == "Conv":
+                            via_conv.add(key)
+                        return True
+        return False
+
+    for name, arr in floats.items():
+        if _strip(name) not in PARAM_SHAPES:
+            attribute(name, arr)
+    # 3) a BatchNorm the exporter fused into its convolution leaves no parameters: identity norm -- but only
+    #    when the graph has no BatchNormalization node in that scope (an unfused BN whose inputs could not be
+    #    attributed must stay missing, so load_onnx_weights raises) and the convolution it follows got both
+    #    its weight and its bias from a Conv node (the fused pair)
+    bn_scopes = {scope_of(nd["name"]) for nd in nodes if nd["op"] == "BatchNormalization"}
     for key in PARAM_SHAPES:
-        if key.endswith(".running_var"):
-            base = key[: -len("running_var")]
-            bn = [base + r for r in ("weight", "bias", "running_mean", "running_var")]
-            if all(k not in out for k in bn):
-                n = PARAM_SHAPES[key][0]
-                out[bn[0]] = np.ones(n, np.float32)
-                out[bn[1]] = np.zeros(n, np.float32)
-                out[bn[2]] = np.zeros(n, np.float32)
-                out[bn[3]] = np.full(n, 1.0 - 1e-5, np.float32)    # 1 / sqrt(var + eps) = 1
+        if not key.endswith(".running_var"):
+            continue
+        base = key[: -len("running_var")]
+        bn = [base + r for r in ("weight", "bias", "running_mean", "running_var")]
+        if any(k in out for k in bn) or base[:-1] in bn_scopes:
+            continue
+        conv = _bn_conv(base[:-1])
+        if conv is None or f"{conv}.weight" not in via_conv or f"{conv}.bias" not in via_conv:
+            continue
+        n = PARAM_SHAPES[key][0]
+        out[bn[0]] = np.ones(n, np.float32)
+        out[bn[1]] = np.zeros(n, np.float32)
+        out[bn[2]] = np.zeros(n, np.float32)
+        out[bn[3]] = np.full(n, 1.0 - 1e-5, np.float32)    # 1 / sqrt(var + eps) = 1
     return out
 
 
+# ---- the flat state layout inside the artifact ----------------------------------------------------------
+# The 2-input graph (configs/streaming_acoustic/config.pbtxt:5-33: signal (B,2400,1) int32, state (B,219729)
+# fp16 -> logprobs, state_next) cuts its ``state`` input into the seven tensors of Tone.forward_for_export
+# (tone/nn/model.py:101-113) with Slice / Split nodes followed by Reshape, and builds ``state_next`` with one
+# Concat along axis 1.  The exporter of that artifact is not in the reference, so instead of
+# assuming its order, the loader reads it from those nodes and compares it with tone_amd.config.STATE_SECTIONS.
+_STATE_PASS = {"Cast", "Identity"}
+_INT64_MAX = (1 << 63) - 1
+
+
+def _const(tensors: dict, name: str):
+    return None if name not in tensors else np.asarray(tensors[name])
+
+
+def _shape_tail(tensors: dict, name: str):
+    """Per-stream shape of a Reshape's constant shape input ([B or -1 or 0, ...] -> the rest), or None."""
+    s = _const(tensors, name)
+    if s is None or s.ndim != 1 or len(s) < 2 or np.any(s[1:] <= 0):
+        return None
+    return tuple(int(x) for x in s[1:])
+
+
+def onnx_state_layout(tensors: dict[str, np.ndarray], nodes: list[dict], state_in: str = "state",
+                      state_out: str = "state_next") -> dict | None:
+    """The flat state layout a graph implements, or None when the graph has no ``state`` input consumer.
+
+    ``input``: the segments the graph cuts from ``state``, sorted by offset: ``(offset, size, shape)`` with
+    ``shape`` the per-stream shape of the Reshape that follows the cut (None when it is not a constant).
+    ``output``: per input of the Concat that produces ``state_next``, in order, ``(size, shape)`` from the
+    constant Reshape / Flatten in front of it (None entries where the graph computes shapes at run time);
+    None when no such Concat is found."""
+    consumers: dict[str, list[tuple[dict, int]]] = {}
+    producer: dict[str, dict] = {}
+    for nd in nodes:
+        for i, x in enumerate(nd["inputs"]):
+            consumers.setdefault(x, []).append((nd, i))
+        for o in nd["outputs"]:
+            producer[o] = nd
+    if state_in not in consumers:
+        return None
+
+    def axis_ok(ax) -> bool:
+        return int(ax) in (1, -1)
+
+    segs: list[list] = []                       # [offset, size, value name]
+    frontier = [(state_in, 0)]
+    seen = set()
+    while frontier:
+        val, depth = frontier.pop()
+        if val in seen or depth > 8:
+            continue
+        seen.add(val)
+        for nd, slot in consumers.get(val, []):
+            if slot != 0:
+                continue
+            op = nd["op"]
+            if op in _STATE_PASS:
+                frontier += [(o, depth + 1) for o in nd["outputs"]]
+            elif op == "Slice":
+                ins = nd["inputs"] + [""] * 5
+                st, en = _const(tensors, ins[1]), _const(tensors, ins[2])
+                ax = _const(tensors, ins[3]) if ins[3] else np.array([1])
+                stp = _const(tensors, ins[4]) if ins[4] else np.array([1])
+                if st is None or en is None or ax is None or stp is None or st.size != 1 or not axis_ok(ax.ravel()[0]) \
+                        or int(stp.ravel()[0]) != 1:
+                    raise ValueError(f"state input: Slice {nd['name'] or '?'} is not a constant unit-step cut along axis 1")
+                a = int(st.ravel()[0])
+                b = min(int(en.ravel()[0]), C.STATE_SIZE)
+                segs.append([a, b - a, nd["outputs"][0]])
+            elif op == "Split":
+                ax = nd["attrs"].get("axis", 0)
+                sizes = nd["attrs"].get("split")
+                if sizes is None and len(nd["inputs"]) > 1 and nd["inputs"][1]:
+                    sz = _const(tensors, nd["inputs"][1])
+                    sizes = None if sz is None else [int(x) for x in sz.ravel()]
+                if not axis_ok(ax) or not sizes:
+                    raise ValueError(f"state input: Split {nd['name'] or '?'} is not a constant split along axis 1")
+                off = 0
+                for s, o in zip(sizes, nd["outputs"]):
+                    segs.append([off, int(s), o])
+                    off += int(s)
+    if not segs:
+        return None
+
+    def reshape_after(val: str, depth: int = 0):
+        for nd, slot in consumers.get(val, []):
+            if nd["op"] in _STATE_PASS and depth < 4:
+                r = reshape_after(nd["outputs"][0], depth + 1)
+                if r is not None:
+                    return r
+            elif nd["op"] == "Reshape" and slot == 0:
+                return _shape_tail(tensors, nd["inputs"][1])
+        return None
+
+    layout_in = sorted((a, s, reshape_after(v)) for a, s, v in segs)
+
+    # state_next: Concat (axis 1) of the flattened next states
+    def size_of(val: str, depth: int = 0):
+        nd = producer.get(val)
+        if nd is None or depth > 6:
+            return None, None
+        if nd["op"] in _STATE_PASS:
+            return size_of(nd["inputs"][0], depth + 1)
+        if nd["op"] == "Reshape":
+            t = _shape_tail(tensors, nd["inputs"][1])
+            if t is not None:
+                if len(t) == 1:                   # [B, n]: the per-stream shape is the one before the flatten
+                    inner = size_of(nd["inputs"][0], depth + 1)[1]
+                    return t[0], inner
+                return int(np.prod(t)), t
+            inner = size_of(nd["inputs"][0], depth + 1)
+            return inner
+        if nd["op"] == "Flatten" and int(nd["attrs"].get("axis", 1)) == 1:
+            return size_of(nd["inputs"][0], depth + 1)
+        return None, None
+
+    out_node = producer.get(state_out)
+    while out_node is not None and out_node["op"] in _STATE_PASS:
+        out_node = producer.get(out_node["inputs"][0])
+    layout_out = None
+    if out_node is not None and out_node["op"] == "Concat" and axis_ok(out_node["attrs"].get("axis", 0)):
+        layout_out = [size_of(x) for x in out_node["inputs"]]
+    return {"input": layout_in, "output": layout_out}
+
+
+def check_state_layout(layout: dict | None, where: str = "model.onnx") -> None:
+    """Compare a graph's state layout (:func:`onnx_state_layout`) with tone_amd.config.STATE_SECTIONS; raise
+    ValueError naming the difference.  The seven segment sizes are distinct, so each cut is identified by its
+    size; a per-stream shape is compared where the graph reshapes with a constant shape."""
+    if layout is None:
+        return
+    want = sorted((off, int(np.prod(shp)), shp, name) for name, (off, shp) in C.STATE_SECTIONS.items())
+    by_size = {w[1]: w[3] for w in want}
+
+    def names(sizes):
+        return " | ".join(by_size.get(s, f"?({s})") if s is not None else "?" for s in sizes)
+
+    got = layout["input"]
+    if [g[1] for g in got] != [w[1] for w in want] or [g[0] for g in got] != [w[0] for w in want]:
+        raise ValueError(
+            f"{where}: the graph cuts its state input as {names([g[1] for g in got])} "
+            f"(offsets {[g[0] for g in got]}); this engine's flat state is {names([w[1] for w in want])} "
+            f"(offsets {[w[0] for w in want]}, tone_amd/config.py). Convert the state (tone_amd.state) or use a "
+            "matching artifact.")
+    for (off, size, shp), (_, _, wshp, name) in zip(got, want):
+        if shp is not None and tuple(shp) != tuple(wshp) and tuple(x for x in shp if x != 1) != tuple(x for x in wshp if x != 1):
+            raise ValueError(f"{where}: state segment {name} at offset {off} is reshaped to {tuple(shp)} in the graph, "
+                             f"{tuple(wshp)} in this engine (a transposed layout inside the segment)")
+    out = layout["output"]
+    if out is not None:
+        sizes = [o[0] for o in out]
+        if all(s is not None for s in sizes) and sizes != [w[1] for w in want]:
+            raise ValueError(f"{where}: the graph concatenates state_next as {names(sizes)}; this engine writes "
+                             f"{names([w[1] for w in want])}")
+        for (size, shp), (_, _, wshp, name) in zip(out, want):
+            if shp is not None and tuple(x for x in shp if x != 1) != tuple(x for x in wshp if x != 1):
+                raise ValueError(f"{where}: next-state segment {name} is flattened from {tuple(shp)} in the graph, "
+                                 f"{tuple(wshp)} in this engine")
+
+
 def load_onnx_weights(path: str | Path):
-    """Parameters of ``model.onnx`` by reference name (raises ValueError naming what is missing)."""
+    """Parameters of ``model.onnx`` by reference name (raises ValueError naming what is missing).  When the
+    graph takes the flat ``state`` input, its state layout is checked against this engine's first
+    (:func:`check_state_layout`)."""
     from .weights import PARAM_SHAPES, normalize_keys
 
     tensors, nodes = read_onnx_graph(path)
+    check_state_layout(onnx_state_layout(tensors, nodes), str(path))
     sd = onnx_state_dict(tensors, nodes)
     missing = [k for k in PARAM_SHAPES if k not in sd]
     if missing:
