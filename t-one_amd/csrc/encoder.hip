@@ -525,9 +525,58 @@ __global__ void __launch_bounds__(256) head_kernel(const float* __restrict__ x, 
   }
 }
 
+// The same for a few rows (the drop-in's B = 1 .. 6 streams): one wave per row, lane l owns k = l + 64 i (six k), W
+// read straight from L2 (no LDS staging, which the 256-row blocks amortise), the 35 partial sums combined by a
+// six-step xor butterfly; then the same log-softmax / greedy / speech-flag epilogue.
+__global__ void __launch_bounds__(256) head_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, float* __restrict__ logp,
+                                                        int32_t* __restrict__ frame_info, int rows) {
+  const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;                                       // wave-uniform
+  const float* xr = x + (int64_t)row * kD;
+  float xv[kD / 64];
+#pragma unroll
+  for (int i = 0; i < kD / 64; ++i) xv[i] = xr[lane + 64 * i];
+  float acc[kVocab];
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < kD / 64; ++i) a = fmaf(w[v * kD + lane + 64 * i], xv[i], a);
+    acc[v] = a;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) {
+    acc[v] = wave_sum(acc[v]) + bias[v];
+    m = fmaxf(m, acc[v]);
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) se += expf(acc[v] - m);
+  const float lse = logf(se);
+  float best = -INFINITY, mine = 0.f;
+  int tok = 0;
+#pragma unroll
+  for (int v = 0; v < kVocab; ++v) {
+    const float lp = acc[v] - m - lse;
+    if (lp > best) { best = lp; tok = v; }
+    if (v == lane) mine = lp;
+  }
+  if (lane < kVocab) logp[(int64_t)row * kVocab + lane] = mine;
+  if (frame_info && lane == 0) {
+    const float sil = expf(acc[kVocab - 2] - m - lse) + expf(acc[kVocab - 1] - m - lse);
+    frame_info[row] = tok | ((sil <= kSilenceThreshold) ? 256 : 0);
+  }
+}
+
 hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows,
                        hipStream_t st) {
   if (rows <= 0) return hipSuccess;
+  if (rows <= 64) {
+    hipLaunchKernelGGL(head_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(head_kernel, dim3((rows + 63) / 64), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
   return hipGetLastError();
 }

@@ -71,9 +71,13 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
   __shared__ float sc[kSub1C], sh[kSub1C];
   __shared__ __half st2[kSub1C * kSub2S * kSub1F];      // sub2 state [c][8][44]: carried in, then next
   __shared__ __attribute__((aligned(16))) float tbuf[8][32 * kSub1C];   // per-wave output tile (32 pos x 32 ch)
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // gridDim.y parts of one stream (small batches, the drop-in's B = 1 call pattern): part y computes the position
+  // tiles y * 8 + wave, + 8 * parts ...; part 0 also writes the sub1 state and the carried x2 rows; with parts > 1
+  // the next sub2 state goes straight to global memory instead of through the LDS image
+  const int b = blockIdx.x, part = blockIdx.y, parts = gridDim.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t srow = s.row_in(b), orow = s.row_out(b);
-  for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) st2[i] = s.in[srow + kOffSub2 + i];
+  if (part == 0)
+    for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) st2[i] = s.in[srow + kOffSub2 + i];
   for (int i = tid; i < kSub1C * kSub1Kt * kKfP; i += 512) {
     const int c = i / (kSub1Kt * kKfP), k = i % (kSub1Kt * kKfP), kt = k / kKfP, kf = k % kKfP;
     wk[c][k] = kf < kSub1Kf ? w1[(c * kSub1Kt + kt) * kSub1Kf + kf] : 0.f;
@@ -87,11 +91,11 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
     const float rms = sqrtf(ssq) * 0.125f;          // * 64^-0.5
     const float y = pre_norm_w[lane] * (v / (rms + kRmsEps));
     x1[(kSub1S + t) * kMels + lane] = y;
-    if (t >= kMelT - kSub1S) s.out[orow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
+    if (part == 0 && t >= kMelT - kSub1S) s.out[orow + kOffSub1 + (t - (kMelT - kSub1S)) * kMels + lane] = __float2half_rn(y);
   }
   float* xb = x2 + (int64_t)b * kSub2In * kSub1F * kSub1C;
   __syncthreads();
-  for (int i = tid; i < kSub1C * kSub2S * kSub1F / 4; i += 512) {   // carried rows -> x2 rows 0..7 (channels-last)
+  for (int i = part == 0 ? tid : 1 << 30; i < kSub1C * kSub2S * kSub1F / 4; i += 512) {   // carried rows -> x2 rows 0..7
     const int c = (4 * i) % kSub1C, rf = (4 * i) / kSub1C;            // 4 channels per thread, 16-byte stores
     const int e = c * kSub2S * kSub1F + rf;
     *reinterpret_cast<float4*>(xb + 4 * i) =
@@ -100,7 +104,7 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
   }
   __syncthreads();                                              // st2 is reused for the next state below
   const int li = lane & 31, lh = lane >> 5;
-  for (int tile = wid; tile * 32 < kPos1; tile += 8) {
+  for (int tile = part * 8 + wid; tile * 32 < kPos1; tile += 8 * parts) {
     const int pos = min(tile * 32 + li, kPos1 - 1);
     const float* xa = x1 + (pos / kSub1F) * kMels + pos % kSub1F + lh;
     const float* wb = &wk[li][lh];
@@ -121,7 +125,11 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
       tw[pl * kSub1C + c] = y;
       if (p >= kPos1) continue;
       const int t = p / kSub1F, f = p % kSub1F;
-      if (t >= kMelT - kSub2S) st2[(c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
+      if (t >= kMelT - kSub2S) {
+        const int e = (c * kSub2S + (t - (kMelT - kSub2S))) * kSub1F + f;
+        if (parts == 1) st2[e] = __float2half_rn(y);
+        else s.out[orow + kOffSub2 + e] = __float2half_rn(y);
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -136,6 +144,7 @@ __global__ void __launch_bounds__(512) sub1_f32_kernel(const float* __restrict__
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+  if (parts > 1) return;
   __syncthreads();
   for (int i = tid; i < kSub1C * kSub2S * kSub1F; i += 512) s.out[orow + kOffSub2 + i] = st2[i];
 }
@@ -268,7 +277,9 @@ static hipError_t launch_sub1_t(const float* feats, StateRef s, const float* pre
     hipLaunchKernelGGL(sub1_bf16_kernel<MT>, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w,
                        static_cast<const uint16_t*>(w1t), scale1, shift1, static_cast<uint16_t*>(x2));
   } else {
-    hipLaunchKernelGGL(sub1_f32_kernel<MT>, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w, w1, scale1, shift1,
+    // a few streams: split each stream's position tiles over parts workgroups (one tile per wave)
+    const int parts = B <= 16 ? (MT * kSub1F / 32 + 1 + 7) / 8 : 1;
+    hipLaunchKernelGGL(sub1_f32_kernel<MT>, dim3(B, parts), dim3(512), 0, st, feats, s, pre_norm_w, w1, scale1, shift1,
                        static_cast<float*>(x2));
   }
   return hipGetLastError();
@@ -629,6 +640,61 @@ __global__ void __launch_bounds__(512) conv2_p3_kernel(const float* __restrict__
       *reinterpret_cast<float4*>(dst + ch) = y;
     }
   }
+}
+
+// a3 conv2 for a few streams in fp32 mode (the drop-in's B = 1 call pattern): conv2_p3 runs 2-3 workgroups per
+// stream, each bound by its own CU's split-MFMA rate (117 us at B = 1, profiles/r03_fp32_b1_step_breakdown.txt).
+// Here a workgroup owns one output row t, 16 output channels and 16 positions f of one stream, its 11 waves take one
+// kernel row kt each (K = 11 kf x 32 channels = 22 steps of 16) on the exact fp32 MFMA v_mfma_f32_16x16x4_f32 (the
+// lane / k map of gemm_sm.hip: lane l loads W[c][k0 + 4 (l >> 4) ..] and x2[row][f + kf][same channels]), and the 11
+// partial sums are added in kt order through LDS before the BatchNorm + SiLU epilogue: 10 x 4 x 3 = 120 workgroups
+// per stream.
+template <int T>
+__global__ void __launch_bounds__(kSub2Kt * 64) conv2_sm_kernel(const float* __restrict__ x2, const float* __restrict__ w2,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, float* __restrict__ flat) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int kIn = (T == make_geom(3200).T ? make_geom(3200) : make_geom(2400)).sub2In;   // input rows per stream
+  __shared__ __attribute__((aligned(16))) float red[(kSub2Kt - 1) * 64 * 4];
+  const int t = blockIdx.x, cb = blockIdx.y, b = blockIdx.z / 3, mbk = blockIdx.z % 3;
+  const int tid = threadIdx.x, lane = tid & 63, kt = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int c = 16 * cb + l16;                                   // A-operand row: output channel
+  const int f = min(16 * mbk + l16, kSub2F - 1);                 // B-operand column: output position (clamped)
+  const float* wr = w2 + (int64_t)c * kConv2K + kt * kSub2Kf * kSub1C + 4 * lg;
+  const float* xr = x2 + (((int64_t)b * kIn + kSub2Stride * t + kt) * kSub1F + f) * kSub1C + 4 * lg;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < 2 * kSub2Kf; ++st) {                     // step = (kf, channel half)
+    const int kf = st >> 1, ch = 16 * (st & 1);
+    const f32x4 w = *reinterpret_cast<const f32x4*>(wr + kf * kSub1C + ch);
+    const f32x4 x = *reinterpret_cast<const f32x4*>(xr + kf * kSub1C + ch);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j], x[j], acc, 0, 0, 0);
+  }
+  if (kt > 0) *reinterpret_cast<f32x4*>(red + ((kt - 1) * 64 + lane) * 4) = acc;
+  __syncthreads();
+  if (kt > 0) return;
+#pragma unroll
+  for (int g = 1; g < kSub2Kt; ++g) acc += *reinterpret_cast<const f32x4*>(red + ((g - 1) * 64 + lane) * 4);
+  const int fo = 16 * mbk + l16;                                 // lane: position fo, channels 16 cb + 4 lg .. + 3
+  if (fo >= kSub2F) return;
+  const int c0 = 16 * cb + 4 * lg;
+  f32x4 y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) y[r] = silu_f(fmaf(acc[r], scale[c0 + r], shift[c0 + r]));
+  *reinterpret_cast<f32x4*>(flat + ((int64_t)b * T + t) * (kSub2F * kSub2C) + fo * kSub2C + c0) = y;
+}
+
+hipError_t launch_conv2_sm(const void* x2, const void* w2, const float* scale, const float* shift, void* flat, int B,
+                           int T, hipStream_t st) {
+  const float* xs = static_cast<const float*>(x2);
+  const float* ws = static_cast<const float*>(w2);
+  float* fl = static_cast<float*>(flat);
+  if (T == 13) hipLaunchKernelGGL((conv2_sm_kernel<13>), dim3(13, 4, 3 * B), dim3(kSub2Kt * 64), 0, st, xs, ws, scale, shift, fl);
+  else if (T == kT) hipLaunchKernelGGL((conv2_sm_kernel<kT>), dim3(kT, 4, 3 * B), dim3(kSub2Kt * 64), 0, st, xs, ws, scale, shift, fl);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 
 hipError_t launch_conv2_p3(const void* x2, const void* w2p, const float* scale, const float* shift, void* flat, int B,

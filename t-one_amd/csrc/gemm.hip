@@ -803,7 +803,7 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   // (FFN up M = 40960: 114 vs 165 us, M = 10240: 37 vs 41; pw1 M = 40960: 42 vs 47; profiles/r03_xs_route_sweep.jsonl)
   const int xblocks = (a.M + 255) / 256;
   if (a.K == 384 && ((epi == EPI_SWIGLU && xblocks >= 40) || (epi == EPI_GLU && xblocks >= 60))) {
-    const hipError_t e = gemm_xs(a, epi, 0, st);
+    const hipError_t e = knobs().xw ? gemm_xw(a, epi, 0, st) : gemm_xs(a, epi, 0, st);
     if (e != hipErrorInvalidValue) return e;   // shape outside gemm_xs's contract: the routes below
   }
   // FFN up: 256 x 256 tiles once there are ~180 of them (M >= 3840 at N = 3072), 256 W x 128 X rows below that
@@ -903,6 +903,9 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     // 15.0), the subsampling Linear (K = 2176) split four ways on 64x64 four-wave tiles (16.9 vs 19.1), the other
     // N = 384 / 1152 projections on 64x32 tiles (6.5 vs 6.8, 7.2 vs 18.6)
     if (a.M <= 64) {
+      // B <= 6 streams: fp32 W streamed straight into registers on the exact fp32 MFMA (gemm_sm.hip)
+      const hipError_t es = gemm_sm(a, epi, st);
+      if (es != hipErrorInvalidValue) return es;
       if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 5, st);
       if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) {
         if (a.K >= 1024 && !a.rowscale && a.ws && a.K % 4 == 0 && (int64_t)4 * a.M * a.N <= a.ws_cap &&
@@ -959,7 +962,9 @@ hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const f
   // per-stream LDS slab kernel (frontend.hip): the 300 ms slab (38 rows, 107 KB) fits, 400 ms (48) does not
   if (bf16 && geo.T == kT) return launch_conv2_bf16(x2, w, scale, shift, flat, B, st);
   // fp32 split mode (frontend.hip): input rows split once per kernel row (conv2_p3)
-  if (w2p) return launch_conv2_p3(x2, w2p, scale, shift, flat, B, geo.T, st);
+  // (B <= 8 streams: conv2_sm, the taps spread over 120 workgroups per stream on the exact fp32 MFMA)
+  if (w2p) return B <= 8 ? launch_conv2_sm(x2, w, scale, shift, flat, B, geo.T, st)
+                         : launch_conv2_p3(x2, w2p, scale, shift, flat, B, geo.T, st);
   GemmArgs a{};
   a.A = x2;
   a.W = w;

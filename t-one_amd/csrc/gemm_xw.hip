@@ -1,0 +1,361 @@
+// X-stationary bf16 GEMM for K = 384 on the 32x32x16 MFMA, with the W ring and the epilogue pipeline running
+// across work items (round 4): FFN up (SwiGLU) and pw1 (GLU) at large batch, bf16 h out.
+//
+// What bounded gemm_xs (gemm_xs.hip, DESIGN.md section 3 "What bounds the K = 384 GEMMs"): the matrix pipe was busy
+// 35 % of the launch because everything else a SIMD issues -- the two waves' SwiGLU epilogues (two quarter-rate
+// transcendentals per output), the W-fragment reads, the LDS-DMA pieces -- shares the SIMD's issue port with the
+// MFMAs, and a v_mfma_f32_16x16x32_bf16 holds that port for 8 of its 16 cycles (MI355X_MICROARCH.md, cycle
+// constants): per 64 x 64 x 384 block of a SIMD, 1536 issue cycles of MFMA holds + ~1300 of epilogue + the reads
+// and DMA against 3072 MFMA cycles.  And each work item (256 X rows, a run of W tiles) began with an exposed X load
+// and ring refill.  Here:
+//   * v_mfma_f32_32x32x16_bf16 (32 cycles, holds the issue port for 8): the same MFMA cycles with half the issue
+//     holds.  Operands: W tile rows as the 32-row A operand (LDS), the wave's 32 X rows as the B operand (registers,
+//     24 K-steps x 8 bf16 = 96 VGPRs).  One 64-row W tile = the g | u 32-row block pair of 32 hidden columns (the
+//     session's 32-row SwiGLU / GLU interleave): acc_g, acc_u (16 regs each) hold g and u of the same (unit, row).
+//   * the A operand's lane l reads W row c(l & 31) of the block, c = swap of bits 2 and 3: D row p of the 32x32
+//     result (p = (r & 3) + 8 (r >> 2) + 4 h for register r, lane half h) then holds unit c(p) = 16 (r >> 3) + 8 h +
+//     (r & 7), so each lane owns 8 consecutive hidden columns in registers 0-7 and 8 more in 8-15: two 16-byte stores
+//     per lane and tile, no lane swaps.  c keeps every ds_read_b128 16-lane group on 16 distinct rows mod 16, so with
+//     chunk c' of row r at slot c' ^ (r & 15) the reads stay conflict-free.
+//   * one flat step sequence per workgroup over all its (item, W tile) pairs: tile s + 2 is DMA'd into ring slot
+//     (s + 2) % 3 at the start of step s across item boundaries, the epilogue of step s - 1 (bias, SwiGLU, bf16,
+//     stores) runs between step s's MFMAs whatever item it belongs to, and the next item's X fragments are loaded
+//     at the end of an item's last step (into the registers that step no longer needs), so no item starts with an
+//     empty ring or a drained epilogue.
+// Work item = (256 X rows, a run of nc W tiles), dealt XCD-contiguously as in gemm_xs.
+#include "common.h"
+#include "kernels.h"
+
+#include "gemm_common.h"
+
+#include <type_traits>
+
+namespace tone {
+namespace {
+
+constexpr int kXwK = 384;                    // K (d_model)
+constexpr int kXwKS = kXwK / 16;             // 32x32x16 K-steps (24)
+constexpr int kXwWaves = 8;                  // two per SIMD
+constexpr int kXwBM = kXwWaves * 32;         // X rows per work item
+constexpr int kXwBN = 64;                    // W rows per tile (g block | u block)
+constexpr int kXwRowB = kXwK * 2;            // bytes per W row
+constexpr int kXwTile = kXwBN * kXwRowB;     // 48 KiB
+constexpr int kXwR = 3;                      // ring depth
+constexpr int kXwP = kXwTile / 1024 / kXwWaves;   // 1 KiB DMA pieces per wave per tile (6)
+constexpr int kXwS = 2;                      // stores per lane per step (the previous step's epilogue)
+
+typedef __bf16 xw_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float xw_f32x16 __attribute__((ext_vector_type(16)));
+typedef float xw_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 xw_bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int xw_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int xw_perm(int r) {   // swap bits 2 and 3 (an involution on 0..31)
+  return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1);
+}
+
+// position of a step in the workgroup's sequence: item, tile j of the item's run, run length n, first W tile t0
+struct XwPos {
+  int item, j, n, t0, mt;
+};
+
+// DBG (XW_ABLATE microbenchmark builds only; 1-16 are timing only, the results are wrong): 1 no epilogue (the MFMAs
+// and fragment reads are then dead code too), 2 no MFMA, 4 no W DMA after the prologue, 16 no W fragment reads, 64 a
+// ping-pong schedule instead of the interleaved one (waves 0-3: half the K-steps, the whole VALU phase, the other
+// half; waves 4-7: VALU phase first), 128 (with 64) the waves 0-3 order for all waves.  Measured at M = 40960
+// (profiles/r04_xw_ablate.jsonl): the ping-pong is 7-8 % slower than the interleaved schedule.
+template <int EPI, bool RS, int DBG = 0>
+__global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, int nc) {
+  static_assert(EPI == EPI_SWIGLU || EPI == EPI_GLU, "SWIGLU / GLU");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kXwR * kXwTile + 4 * kBiasMax];
+  float* sbias = reinterpret_cast<float*>(lds + kXwR * kXwTile);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int nwt = p.N / kXwBN, ntm = (p.M + kXwBM - 1) / kXwBM, nch = (nwt + nc - 1) / nc;
+  const int items = ntm * nch;
+  const int nxb = gridDim.x >> 3, xcd = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int q = (items + 7) >> 3, ibeg = xcd * q, iend = min(items, ibeg + q);
+  if (ibeg + jb >= iend) return;                                  // workgroup-uniform
+
+  for (int i = tid; i < p.N; i += kXwWaves * 64) sbias[i] = p.bias ? p.bias[i] : 0.f;
+  __syncthreads();                                                // no DMA in flight yet
+
+  const uint16_t* __restrict__ X = static_cast<const uint16_t*>(p.A);
+  const uint8_t* __restrict__ Wb = static_cast<const uint8_t*>(p.W);
+  uint16_t* __restrict__ Cout = static_cast<uint16_t*>(p.C);
+
+  auto pos_of = [&](int item) {
+    XwPos ps;
+    ps.item = item;
+    ps.j = 0;
+    ps.mt = item / nch;
+    const int ch = item - ps.mt * nch;
+    ps.t0 = ch * nc;
+    ps.n = min(nwt, ps.t0 + nc) - ps.t0;
+    return ps;
+  };
+  auto advance = [&](XwPos& ps) {
+    if (++ps.j == ps.n) ps = pos_of(ps.item + nxb);
+  };
+  int total = 0;
+  for (int it = ibeg + jb; it < iend; it += nxb) total += pos_of(it).n;
+
+  // DMA of W tile t into ring slot sl: wave w moves pieces 6 w .. 6 w + 5; lane i of piece pc lands at linear 16-byte
+  // slot 64 pc + i of the tile = (row, slot) with 48 slots per row, fetching chunk slot ^ (row & 15) of that row
+  uint32_t doff[kXwP];
+#pragma unroll
+  for (int i = 0; i < kXwP; ++i) {
+    const int pc = wid * kXwP + i, lin = pc * 64 + lane, row = lin / 48, slot = lin % 48;
+    doff[i] = (uint32_t)(row * kXwRowB + ((slot ^ (row & 15)) << 4));
+  }
+  auto dma_piece = [&](int t, int sl, int i) __attribute__((always_inline)) {
+    const uint8_t* src = Wb + (int64_t)t * kXwTile;
+    uint8_t* base = lds + sl * kXwTile + wid * kXwP * 1024;
+    (void)src;
+    (void)base;
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src + doff[i], base + i * 1024, 16, 0, 0);
+#endif
+  };
+  auto dma = [&](int t, int sl) {
+#pragma unroll
+    for (int i = 0; i < kXwP; ++i) dma_piece(t, sl, i);
+  };
+  // A-operand reads: lane row c(lr) of the g block, the same of the u block 32 rows on; chunk 2 ks + lh
+  const int ra = xw_perm(lr);
+  const uint32_t roff = (uint32_t)(ra * kXwRowB), rsw = (uint32_t)(ra & 15);
+  uint32_t soff[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) soff[k] = roff + ((((uint32_t)(2 * k + lh)) ^ rsw) << 4);
+
+  xw_bf16x8 xf[kXwKS];
+  auto xload = [&](const XwPos& ps) {
+    const int64_t row = min(ps.mt * kXwBM + wid * 32 + lr, p.M - 1);
+    const uint16_t* xr = X + row * p.lda + 8 * lh;
+#pragma unroll
+    for (int ks = 0; ks < kXwKS; ++ks) xf[ks] = *reinterpret_cast<const xw_bf16x8*>(xr + 16 * ks);
+  };
+  auto row_inv = [&]() {
+    if constexpr (RS) {
+      float ss = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < kXwKS; ++ks) ss = sumsq8(xf[ks], ss);
+      ss += __shfl_xor(ss, 32, 64);
+      return 1.0f / (sqrtf(ss) * p.inv_sqrt_k + kRmsEps);
+    } else {
+      return 1.0f;
+    }
+  };
+
+  xw_f32x16 acc[2][2];       // [buffer][g, u]
+  uint32_t po[8];            // packed bf16 pairs of the epilogue in flight
+  // epilogue part k (registers 2k, 2k + 1) of the step held in buffer b: W tile t, output row mrow, row factor inv
+  auto epi_part = [&](int b, int t, int64_t mrow, float inv, int k) __attribute__((always_inline)) {
+    const int u = 16 * (k >> 2) + 8 * lh + 2 * (k & 3);              // hidden column of register 2k within the tile
+    const xw_f32x2 bg = *reinterpret_cast<const xw_f32x2*>(sbias + kXwBN * t + u);
+    const xw_f32x2 bu = *reinterpret_cast<const xw_f32x2*>(sbias + kXwBN * t + 32 + u);
+    float y[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {   // scalar fp32 (packed f32 VALU beside MFMAs costs more than two plain ops)
+      const float g = fmaf(acc[b][0][2 * k + e], inv, bg[e]);
+      const float v = fmaf(acc[b][1][2 * k + e], inv, bu[e]);
+      const float z = (EPI == EPI_SWIGLU) ? g : v;               // the sigmoid's argument
+      const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
+      y[e] = (EPI == EPI_SWIGLU) ? g * sg * v : g * sg;
+    }
+    po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{y[0], y[1]}, xw_bf16x2));
+    if ((k & 3) == 3) {   // registers 0-7 / 8-15 done: 8 consecutive hidden columns, one 16-byte store
+      const xw_u32x4 w = {po[k - 3], po[k - 2], po[k - 1], po[k]};
+      *reinterpret_cast<xw_u32x4*>(Cout + mrow * p.ldc + 32 * t + 16 * (k >> 2) + 8 * lh) = w;
+    }
+  };
+
+  // ---- prologue: first item's X, ring steps 0 and 1 ------------------------------------------------------------
+  // Every run has an even length (gemm_xw picks nc among the even divisors of N / 64), so a run's steps use the
+  // accumulator buffers 0, 1, ..., 1: the run's first step (X wait, row factors) and last step (next X load) are
+  // peeled, and the compiler sees the X loads pending only on the path into a first step -- one explicit wait
+  // there, no wait on X anywhere else.
+  XwPos cur = pos_of(ibeg + jb);
+  XwPos ahead = cur;
+  xload(cur);
+  dma(cur.t0 + cur.j, 0);
+  advance(ahead);
+  if (total > 1) dma(ahead.t0 + ahead.j, 1);
+  advance(ahead);                                                 // ahead = step 2
+  int s = 0;
+  float inv = 1.f;
+  int64_t mrow = 0;
+  int pt = 0;                                                     // previous step's W tile, row, row factor
+  int64_t prow = 0;
+  float pinv = 1.f;
+
+  auto step = [&](auto Bc, auto Fc, auto Lc) __attribute__((always_inline)) {
+    constexpr int b = decltype(Bc)::value;
+    constexpr bool first = decltype(Fc)::value, last = decltype(Lc)::value;
+    const int t = cur.t0 + cur.j;
+    if constexpr (first) {
+      // the run's X loads (issued last in the previous step, or in the prologue) are the youngest ops: vmcnt(0),
+      // as a builtin so the compiler's own wait counters see it
+      __builtin_amdgcn_s_waitcnt(0x0F70);                         // vmcnt(0) expcnt(7) lgkmcnt(15)
+    } else {
+      // ring slot s landed: step s's DMA went out one piece at a time during step s - 2 (every four K-steps, or
+      // between the epilogue parts of the ping-pong's VALU phase), its last piece before that step's second store;
+      // younger ops: that store, step s - 1's pieces (tile s + 1) and its two stores
+      const int younger = (s >= 3) + (s + 1 < total ? kXwP : 0) + kXwS * (s >= 2);
+      if (younger == 1 + kXwP + kXwS) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else vmcnt_dyn(younger);
+    }
+    barrier_lds();                                                // ... for every wave; slot (s + 2) % 3 free
+    if constexpr (first) {
+      inv = row_inv();
+      mrow = min(cur.mt * kXwBM + wid * 32 + lr, p.M - 1);
+    }
+    const bool dma_next = s + 2 < total && !(DBG & 4);
+    const int t2 = ahead.t0 + ahead.j, sl2 = (s + 2) % kXwR;
+    const uint8_t* base = lds + (s % kXwR) * kXwTile;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[b][i][r] = 0.f;
+    // W fragments two K-steps ahead of the MFMAs that use them (three register sets)
+    xw_bf16x8 wf[3][2];
+    auto rdw = [&](int ks, xw_bf16x8(&w)[2]) __attribute__((always_inline)) {
+      if constexpr ((DBG & 16) != 0) {
+        w[0] = xf[ks];
+        w[1] = xf[(ks + 1) % kXwKS];
+      } else {
+        // chunk 2 ks + lh at slot (2 ks + lh) ^ rsw: the XOR touches bits 0-3 only, so the slot is 16 (ks >> 3) plus
+        // one of eight per-lane offsets -- eight address registers, the rest immediate offsets
+        const uint8_t* a = base + soff[ks & 7] + 256 * (ks >> 3);
+        w[0] = *reinterpret_cast<const xw_bf16x8*>(a);
+        w[1] = *reinterpret_cast<const xw_bf16x8*>(a + 32 * kXwRowB);
+      }
+    };
+    const bool epi = s > 0 && !(DBG & 1);
+    // K-steps k0 .. k1 - 1, fragments read two steps ahead within the range (none live across a VALU phase)
+    auto mfmas = [&](int k0, int k1) __attribute__((always_inline)) {
+      rdw(k0, wf[k0 % 3]);
+      rdw(k0 + 1, wf[(k0 + 1) % 3]);
+#pragma unroll
+      for (int ks = k0; ks < k1; ++ks) {
+        xw_bf16x8(&cw)[2] = wf[ks % 3];
+        if (ks + 2 < k1) rdw(ks + 2, wf[(ks + 2) % 3]);
+        if constexpr ((DBG & 2) != 0) {
+          asm volatile("" ::"v"(cw[0]), "v"(cw[1]), "v"(xf[ks]));
+        } else {
+          acc[b][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cw[0], xf[ks], acc[b][0], 0, 0, 0);
+          acc[b][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cw[1], xf[ks], acc[b][1], 0, 0, 0);
+        }
+        if constexpr ((DBG & 64) == 0) {   // interleaved schedule: DMA piece / epilogue part between the MFMAs
+          if (dma_next && ks % 4 == 2) dma_piece(t2, sl2, ks / 4);
+          if (epi && ks % 3 == 1) epi_part(b ^ 1, pt, prow, pinv, ks / 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // the VALU phase: the previous step's epilogue (8 parts) with this step's 6 DMA pieces (tile s + 2) between them
+    auto valu_phase = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (epi) epi_part(b ^ 1, pt, prow, pinv, k);
+        if (k < kXwP && dma_next) dma_piece(t2, sl2, k);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if constexpr ((DBG & 64) == 0) {
+      mfmas(0, kXwKS);
+    } else {
+      // ping-pong between the two waves of a SIMD (waves w and w + 4): waves 0-3 run half the K-steps, then their VALU
+      // phase, then the other half; waves 4-7 their VALU phase first -- so one wave's epilogue issues while its
+      // partner's MFMAs hold the matrix pipe, instead of both waves interleaving VALU and MFMA at K-step grain
+      if (wid < 4 || (DBG & 128)) {
+        mfmas(0, kXwKS / 2);
+        valu_phase();
+        mfmas(kXwKS / 2, kXwKS);
+      } else {
+        valu_phase();
+        mfmas(0, kXwKS);
+      }
+    }
+    pt = t;
+    prow = mrow;
+    pinv = inv;
+    advance(cur);
+    advance(ahead);
+    ++s;
+    if constexpr (last) {
+      if (s < total) xload(cur);                                  // next run's X into the registers just freed
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T = std::true_type;
+  using F = std::false_type;
+  for (int it = ibeg + jb; it < iend; it += nxb) {                // cur is at (it, 0)
+    const int n = cur.n;
+    step(I0{}, T{}, F{});
+    for (int j = 1; j < n - 1; j += 2) {
+      step(I1{}, F{}, F{});
+      step(I0{}, F{}, F{});
+    }
+    step(I1{}, F{}, T{});
+  }
+  // the last step's epilogue (buffer 1: runs have even lengths)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) epi_part(1, pt, prow, pinv, k);
+}
+
+// W tiles per work item: among the even divisors of the W tile count (runs of even length), the one minimising
+// rounds x (run + 1.5), 1.5 tiles being the per-item X load and ring refill that the pipeline does not hide
+inline int xw_run_length(int x_blocks, int w_tiles, int cus = 256) {
+  int best = 0;
+  double best_cost = 1e30;
+  for (int c = 2; c <= w_tiles; c += 2) {
+    if (w_tiles % c) continue;
+    const int64_t items = (int64_t)x_blocks * (w_tiles / c);
+    const double cost = (double)((items + cus - 1) / cus) * (c + 1.5);
+    if (cost < best_cost) { best_cost = cost; best = c; }
+  }
+  return best;
+}
+
+template <int EPI>
+hipError_t launch_xw(const GemmArgs& a, int nc, hipStream_t st) {
+  const int items = ((a.M + kXwBM - 1) / kXwBM) * ((a.N / kXwBN + nc - 1) / nc);
+  int grid = 256;
+  const int need = (items + 7) / 8 * 8;
+  if (grid > need) grid = need;
+#ifdef XW_ABLATE
+  if constexpr (EPI == EPI_SWIGLU) {
+    switch (a.rowscale ? a.dbg : 0) {
+#define XW_D(d) case d: hipLaunchKernelGGL((gemm_xw_kernel<EPI, true, d>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc); return hipGetLastError();
+      XW_D(1) XW_D(2) XW_D(3) XW_D(4) XW_D(16) XW_D(19) XW_D(64) XW_D(192)
+#undef XW_D
+      default: break;
+    }
+  }
+#endif
+  if (a.rowscale) hipLaunchKernelGGL((gemm_xw_kernel<EPI, true>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc);
+  else hipLaunchKernelGGL((gemm_xw_kernel<EPI, false>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// nc = W tiles per work item, an even divisor of N / 64 (0: xw_run_length); SWIGLU / GLU with bf16 output only
+hipError_t gemm_xw(const GemmArgs& a, int epi, int nc, hipStream_t st) {
+  if (!a.a_bf16 || !a.c_bf16 || a.K != kXwK || a.N % kXwBN || a.N > kBiasMax || a.M <= 0 || a.rpg || a.lda % 8 ||
+      a.ldc % 8 || a.k_split || a.C2)
+    return hipErrorInvalidValue;
+  const int nwt = a.N / kXwBN, ntm = (a.M + kXwBM - 1) / kXwBM;
+  if (nc <= 0) nc = xw_run_length(ntm, nwt);
+  if (nc < 2 || nc % 2 || nwt % nc) return hipErrorInvalidValue;   // runs of even length (see the kernel)
+  switch (epi) {
+    case EPI_SWIGLU: return launch_xw<EPI_SWIGLU>(a, nc, st);
+    case EPI_GLU: return launch_xw<EPI_GLU>(a, nc, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tone

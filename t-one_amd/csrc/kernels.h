@@ -14,6 +14,7 @@ namespace tone {
 struct Knobs {
   int x3_prio;         // TONE_X3_PRIO=0: no static priority in gemm_x3 (default on)
   int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand
+  int xw;              // TONE_XW=1: route the X-stationary bf16 GEMMs to gemm_xw (A/B, round 4)
 };
 const Knobs& knobs();
 
@@ -108,6 +109,9 @@ hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // X-stationary bf16 GEMM for K = 384 (gemm_xs.hip): X rows in registers, W tiles streamed through an LDS ring,
 // epilogue overlapped with the next tile's MFMAs; SWIGLU / GLU / STORE (bf16 out); nc = W tiles per work item (0: auto)
 hipError_t gemm_xs(const GemmArgs& a, int epi, int nc, hipStream_t st);
+// the same on v_mfma_f32_32x32x16_bf16 with the W ring and epilogue pipeline running across work items
+// (gemm_xw.hip): SWIGLU / GLU, bf16 out; nc = W tiles per work item (0: auto)
+hipError_t gemm_xw(const GemmArgs& a, int epi, int nc, hipStream_t st);
 // W-stationary bf16 GEMM for K = 384 (gemm_ws.hip, microbenchmark build only -- measured no faster than gemm_xs,
 // DESIGN.md section 3): a 192-row W slice per workgroup held in LDS for the whole launch, X streamed by each wave
 // straight into registers; SWIGLU / GLU / STORE; variant 0 / 1 (see there)
@@ -116,6 +120,9 @@ hipError_t gemm_ws(const GemmArgs& a, int epi, int variant, hipStream_t st);
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3
 hipError_t gemm_x3(const GemmArgs& a, int epi, int variant, hipStream_t st);
+// exact-fp32 projections for M <= 64 (gemm_sm.hip): fp32 W streamed into registers, v_mfma_f32_16x16x4_f32, K split
+// over the waves of a 16-column workgroup; STORE / RESID / SWIGLU / GLU, fp32 in and out
+hipError_t gemm_sm(const GemmArgs& a, int epi, hipStream_t st);
 // the same with the K range split over nsplit workgroups (partials in a.ws, fixed-order combine; gemm.hip)
 hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // the same arithmetic with fp32 W and X streamed through a K-tile ring (gemm_t.hip gemm_r3_kernel); needs a.W fp32
@@ -136,6 +143,10 @@ hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale
 hipError_t launch_conv2_p3(const void* x2, const void* w2p, const float* scale, const float* shift, void* flat, int B,
                            int T, hipStream_t st);
 void conv2_p3_pack(const uint16_t* planes, uint16_t* w2p);
+// a3 conv2 in fp32 mode for a few streams: exact fp32 MFMA, one workgroup per (row, 16 channels, 16 positions),
+// kernel rows over its 11 waves (frontend.hip); w2 fp32 [64][3872] tap-major
+hipError_t launch_conv2_sm(const void* x2, const void* w2, const float* scale, const float* shift, void* flat, int B,
+                           int T, hipStream_t st);
 
 // a2 log-mel on the fp32 MFMA: power spectrum GEMM over overlapping windows, then filterbank GEMM
 // with the log / fp16 epilogue.  wave [B][2480] fp32 (from launch_mel_prep).

@@ -296,7 +296,8 @@ int main(int argc, char** argv) {
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
-      return vv <= -200 ? gemm_ws(a, epi, -200 - vv, 0)   // -200 / -201: gemm_ws variant 0 / 1
+      return vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
+             : vv <= -200 ? gemm_ws(a, epi, -200 - vv, 0)   // -200 / -201: gemm_ws variant 0 / 1
              : vv <= -10 ? gemm_xs(a, epi, -10 - vv, 0)      // -10: gemm_xs auto run length, -10 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
              : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
