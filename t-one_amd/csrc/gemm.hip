@@ -800,11 +800,13 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   // large batches: the persistent transposed-orientation kernels (gemm_t.hip, tools/gemm_bench sweep)
   const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
   // K = 384 paired projections from 40 (SwiGLU) / 60 (GLU) blocks of 256 rows up: the X-stationary kernel
-  // (FFN up M = 40960: 114 vs 165 us, M = 10240: 37 vs 41; pw1 M = 40960: 42 vs 47; profiles/r03_xs_route_sweep.jsonl)
+  // (round 3's gemm_xs: FFN up M = 40960: 114 vs 165 us for gemm_t, M = 10240: 37 vs 41; pw1 M = 40960: 42 vs 47,
+  // profiles/r03_xs_route_sweep.jsonl; round 4's gemm_xw 1.8 % / 3 % below gemm_xs in the bf16 B = 4096 step,
+  // profiles/r04_xw_step_ab.json)
   const int xblocks = (a.M + 255) / 256;
   if (a.K == 384 && ((epi == EPI_SWIGLU && xblocks >= 40) || (epi == EPI_GLU && xblocks >= 60))) {
-    const hipError_t e = knobs().xw ? gemm_xw(a, epi, 0, st) : gemm_xs(a, epi, 0, st);
-    if (e != hipErrorInvalidValue) return e;   // shape outside gemm_xs's contract: the routes below
+    const hipError_t e = gemm_xw(a, epi, 0, st);
+    if (e != hipErrorInvalidValue) return e;   // shape outside gemm_xw's contract: the routes below
   }
   // FFN up: 256 x 256 tiles once there are ~180 of them (M >= 3840 at N = 3072), 256 W x 128 X rows below that
   // down to ~200 tiles (M = 2560: 14.5 vs 20.2 us; tools/gemm_bench, profiles/r02_ffnup_route.jsonl)

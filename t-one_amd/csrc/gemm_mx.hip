@@ -465,8 +465,8 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// X-stationary MXFP8 GEMM for K = 384 (FFN up + SwiGLU -> MXFP8 h, q|k|v STORE), the fp8 form of gemm_xs
-// (gemm_xs.hip): each wave keeps its 32 X rows x 384 e4m3 in registers (48 VGPRs) with their E8M0 scales and
+// X-stationary MXFP8 GEMM for K = 384 (FFN up + SwiGLU -> MXFP8 h, q|k|v STORE), the fp8 form of round 3's bf16
+// gemm_xs (now gemm_xw.hip): each wave keeps its 32 X rows x 384 e4m3 in registers (48 VGPRs) with their E8M0 scales and
 // row factors, W tiles of 64 rows x 384 B (24 KiB) stream through a 4-deep LDS ring (chunk c of row r at slot
 // c ^ ((r >> 1) & 7), the mx_swz map on 384-byte rows: conflict-free for both ds_read_b128 of a fragment), the
 // W scales of the whole matrix sit in LDS for the launch, and the accumulators are double-buffered so tile

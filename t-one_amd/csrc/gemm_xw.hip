@@ -1,28 +1,25 @@
 // X-stationary bf16 GEMM for K = 384 on the 32x32x16 MFMA, with the W ring and the epilogue pipeline running
-// across work items (round 4): FFN up (SwiGLU) and pw1 (GLU) at large batch, bf16 h out.
+// across work items (round 4; replaces round 3's gemm_xs): FFN up (SwiGLU) and pw1 (GLU) at large batch, bf16 h out.
 //
-// What bounded gemm_xs (gemm_xs.hip, DESIGN.md section 3 "What bounds the K = 384 GEMMs"): the matrix pipe was busy
-// 35 % of the launch because everything else a SIMD issues -- the two waves' SwiGLU epilogues (two quarter-rate
-// transcendentals per output), the W-fragment reads, the LDS-DMA pieces -- shares the SIMD's issue port with the
-// MFMAs, and a v_mfma_f32_16x16x32_bf16 holds that port for 8 of its 16 cycles (MI355X_MICROARCH.md, cycle
-// constants): per 64 x 64 x 384 block of a SIMD, 1536 issue cycles of MFMA holds + ~1300 of epilogue + the reads
-// and DMA against 3072 MFMA cycles.  And each work item (256 X rows, a run of W tiles) began with an exposed X load
-// and ring refill.  Here:
-//   * v_mfma_f32_32x32x16_bf16 (32 cycles, holds the issue port for 8): the same MFMA cycles with half the issue
-//     holds.  Operands: W tile rows as the 32-row A operand (LDS), the wave's 32 X rows as the B operand (registers,
-//     24 K-steps x 8 bf16 = 96 VGPRs).  One 64-row W tile = the g | u 32-row block pair of 32 hidden columns (the
-//     session's 32-row SwiGLU / GLU interleave): acc_g, acc_u (16 regs each) hold g and u of the same (unit, row).
+//   * each of the 8 waves (two per SIMD) keeps its 32 X rows x 384 K in registers as the B operand of
+//     v_mfma_f32_32x32x16_bf16 (24 K-steps x 8 bf16 = 96 VGPRs); W tiles of 64 rows x 384 (48 KiB) stream through a
+//     3-deep LDS ring by global_load_lds_dwordx4 and are read as the 32-row A operand.  One 64-row W tile = the g | u
+//     32-row block pair of 32 hidden columns (the session's 32-row SwiGLU / GLU interleave): acc_g, acc_u (16
+//     registers each) hold g and u of the same (unit, row);
 //   * the A operand's lane l reads W row c(l & 31) of the block, c = swap of bits 2 and 3: D row p of the 32x32
 //     result (p = (r & 3) + 8 (r >> 2) + 4 h for register r, lane half h) then holds unit c(p) = 16 (r >> 3) + 8 h +
 //     (r & 7), so each lane owns 8 consecutive hidden columns in registers 0-7 and 8 more in 8-15: two 16-byte stores
 //     per lane and tile, no lane swaps.  c keeps every ds_read_b128 16-lane group on 16 distinct rows mod 16, so with
-//     chunk c' of row r at slot c' ^ (r & 15) the reads stay conflict-free.
+//     chunk c' of row r at slot c' ^ (r & 15) the reads stay conflict-free;
 //   * one flat step sequence per workgroup over all its (item, W tile) pairs: tile s + 2 is DMA'd into ring slot
-//     (s + 2) % 3 at the start of step s across item boundaries, the epilogue of step s - 1 (bias, SwiGLU, bf16,
-//     stores) runs between step s's MFMAs whatever item it belongs to, and the next item's X fragments are loaded
-//     at the end of an item's last step (into the registers that step no longer needs), so no item starts with an
-//     empty ring or a drained epilogue.
-// Work item = (256 X rows, a run of nc W tiles), dealt XCD-contiguously as in gemm_xs.
+//     (s + 2) % 3 during step s (one piece every four K-steps) across item boundaries, the epilogue of step s - 1
+//     (bias, SwiGLU, bf16, stores) runs between step s's MFMAs whatever item it belongs to, and the next item's X
+//     fragments are loaded at the end of an item's last step (peeled, so the compiler waits for them only there).
+// Measured (profiles/r04_xw_*): 116-125 us at M = 40960 in the microbenchmark (gemm_xs 116-129), 1.8 % (FFN up) and
+// 3 % (pw1) below gemm_xs inside the bf16 B = 4096 step.  Ablations: without MFMAs 74-80 us, without MFMAs and
+// epilogue 50-52, DMA / X loads / barriers alone 33-37; a ping-pong schedule (one wave's whole epilogue under its
+// partner's MFMAs) 7-8 % slower; SQ counters: the matrix pipe busy 38 % of the launch at 1.96 GHz (gemm_xs 32 %).
+// Work item = (256 X rows, a run of nc W tiles), dealt XCD-contiguously.
 #include "common.h"
 #include "kernels.h"
 

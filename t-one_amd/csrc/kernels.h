@@ -14,7 +14,6 @@ namespace tone {
 struct Knobs {
   int x3_prio;         // TONE_X3_PRIO=0: no static priority in gemm_x3 (default on)
   int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand
-  int xw;              // TONE_XW=1: route the X-stationary bf16 GEMMs to gemm_xw (A/B, round 4)
 };
 const Knobs& knobs();
 
@@ -58,7 +57,7 @@ struct GemmArgs {
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
 
-// W tiles per work item of the X-stationary kernels (gemm_xs, gemm_xs8: one 256-row X block, one workgroup per
+// W tiles per work item of the X-stationary MXFP8 kernel (gemm_xs8: one 256-row X block, one workgroup per
 // CU): the run length minimising rounds x (run + 3), 3 tiles being the per-item cost of loading the X fragments and
 // draining the last tile's epilogue; ties go to the longer run (profiles/r03_xs_route_sweep.jsonl)
 inline int xs_run_length(int x_blocks, int w_tiles, int cus = 256) {
@@ -106,16 +105,10 @@ hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
 // persistent transposed-orientation bf16 GEMM (gemm_t.hip); variant = tile shape, see there
 hipError_t gemm_t(const GemmArgs& a, int epi, int variant, hipStream_t st);
-// X-stationary bf16 GEMM for K = 384 (gemm_xs.hip): X rows in registers, W tiles streamed through an LDS ring,
-// epilogue overlapped with the next tile's MFMAs; SWIGLU / GLU / STORE (bf16 out); nc = W tiles per work item (0: auto)
-hipError_t gemm_xs(const GemmArgs& a, int epi, int nc, hipStream_t st);
-// the same on v_mfma_f32_32x32x16_bf16 with the W ring and epilogue pipeline running across work items
-// (gemm_xw.hip): SWIGLU / GLU, bf16 out; nc = W tiles per work item (0: auto)
+// X-stationary bf16 GEMM for K = 384 (gemm_xw.hip): each wave's 32 X rows in registers, W tiles streamed through an
+// LDS ring, v_mfma_f32_32x32x16_bf16, the ring and the epilogue pipeline running across work items; SWIGLU / GLU,
+// bf16 out; nc = W tiles per work item (0: auto)
 hipError_t gemm_xw(const GemmArgs& a, int epi, int nc, hipStream_t st);
-// W-stationary bf16 GEMM for K = 384 (gemm_ws.hip, microbenchmark build only -- measured no faster than gemm_xs,
-// DESIGN.md section 3): a 192-row W slice per workgroup held in LDS for the whole launch, X streamed by each wave
-// straight into registers; SWIGLU / GLU / STORE; variant 0 / 1 (see there)
-hipError_t gemm_ws(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // exact-fp32 MFMA projections with an in-workgroup K split (gemm_t.hip); variant = tile shape
 hipError_t gemm_f32t(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // fp32 operands on the bf16 MFMA by exact 3-way bf16 splitting (6 products; gemm_t.hip); needs a.W3

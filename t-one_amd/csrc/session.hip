@@ -33,7 +33,6 @@ const Knobs& knobs() {
     Knobs r;
     r.x3_prio = env("TONE_X3_PRIO", 1) != 0;
     r.fp8_normq = env("TONE_FP8_NORMQ", 1) != 0;
-    r.xw = env("TONE_XW", 0);
     return r;
   }();
   return k;

@@ -284,7 +284,7 @@ int main(int argc, char** argv) {
     a.order_n = fl & 1;
     a.nt_store = (fl >> 1) & 1;
     a.dbg = (fl >> 2) & 255;   // gemm_t: 1 no epilogue, 2 no MFMA, 4 no DMA; gemm_r3: see gemm_t.hip
-    if (vv <= -10 && getenv("XSDBG")) a.dbg = atoi(getenv("XSDBG"));   // gemm_xs ablations
+    if (vv <= -300 && getenv("XSDBG")) a.dbg = atoi(getenv("XSDBG"));   // gemm_xw ablations
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
     const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 50) || (v >= 50 && v < 90);
@@ -297,8 +297,6 @@ int main(int argc, char** argv) {
     a.c_bf16 = f32 ? 0 : cbf;
     auto launch = [&]() {
       return vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
-             : vv <= -200 ? gemm_ws(a, epi, -200 - vv, 0)   // -200 / -201: gemm_ws variant 0 / 1
-             : vv <= -10 ? gemm_xs(a, epi, -10 - vv, 0)      // -10: gemm_xs auto run length, -10 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
              : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
