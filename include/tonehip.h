@@ -130,9 +130,11 @@ double tone_session_kernel_us(const tone_session *s, const char *family, int64_t
 /* ---- diagnostics (parity localisation; not needed for serving) ------------------------------
  * tone_session_debug_stop: end the step early -- stage 0 after the log-mel front end, 1 after the
  * subsampling (pre-encode + out_norm), 2 + L after Conformer layer L (incl. reduction/upsampling
- * at L = 6 / 14); -1 (default) runs the whole step.  Requires graph mode off.
- * tone_session_debug_read: copy an internal fp32 activation buffer ("feats", "x2", "flat", "rA",
- * "rB") of the last step to host memory. */
+ * at L = 6 / 14), 100 + L after layer L's pw2 (fp8: FFN2's MXFP8 operand made); -1 (default) runs
+ * the whole step.  Requires graph mode off.
+ * tone_session_debug_read: copy an internal buffer of the last step to host memory: fp32 activations
+ * ("feats", "x2", "flat", "rA", "rB"), fp8 mode's next MX GEMM operand ("a8" e4m3 [rows][384], "a8s"
+ * E8M0 [rows][12], "ss8" fp32 sum-of-squares slab [rows][12]). */
 int tone_session_debug_stop(tone_session *s, int stage);
 int tone_session_debug_read(tone_session *s, const char *buffer, void *host_dst, int64_t bytes);
 

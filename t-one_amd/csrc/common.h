@@ -102,6 +102,25 @@ __device__ __forceinline__ float exp2i(int ebiased) {
   return __uint_as_float((uint32_t)(254 - ebiased) << 23);
 }
 
+// fp8 mode: the folded-RMSNorm row factor of an MXFP8 GEMM operand comes from a sum-of-squares slab, kSsSlots floats
+// per row, the sum of the row's squared bf16 values split over 32-column slots: a producer that sees the whole row
+// (quant_mx, the fused rmsnorm) writes {ss, 0, ...}, a RESID GEMM epilogue the partial sum of each 32-column slot
+// range its workgroup / wave covers (zeros in the slots it covers without a sum); the consumer adds the slots in a
+// fixed order (three 4-slot groups) -- {ss, 0, ...} gives ss exactly
+constexpr int kSsSlots = 12;   // 384 / 32
+__device__ __forceinline__ float mx_row_inv(const float* __restrict__ ss_row) {
+  const float4 a = reinterpret_cast<const float4*>(ss_row)[0];
+  const float4 b = reinterpret_cast<const float4*>(ss_row)[1];
+  const float4 c = reinterpret_cast<const float4*>(ss_row)[2];
+  const float ss = (((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w))) + ((c.x + c.y) + (c.z + c.w));
+  return 1.0f / (sqrtf(ss) * 0.05103103630798288f + kRmsEps);   // 384^-0.5
+}
+// 4 floats -> 4 e4m3 bytes (one dword) with the block's inverse scale, saturating, NaN kept
+__device__ __forceinline__ uint32_t quant4(float a, float b, float c, float d, float inv) {
+  uint32_t w = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(a * inv), sat_e4m3(b * inv), 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(c * inv), sat_e4m3(d * inv), (int)w, true);
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform n known only at run time (a scalar branch to the immediate form)
 __device__ __forceinline__ void vmcnt_dyn(int n) {
   switch (n) {

@@ -14,7 +14,7 @@ constexpr float kInvSqrtD = 0.05103103630798288f;   // 384^-0.5 (submodules.py:5
 __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, const float* __restrict__ w, int rows,
                                                       uint16_t* __restrict__ shadow, int64_t plane,
                                                       uint8_t* __restrict__ q8, uint8_t* __restrict__ s8,
-                                                      float* __restrict__ inv8) {
+                                                      float* __restrict__ ss8) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -49,15 +49,15 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, con
       if ((lane & 31) == 0) s8[(int64_t)row * (kD / 32) + 2 * i + (lane >> 5)] = (uint8_t)e;
     }
   }
-  if (q8 && inv8) {
+  if (q8 && ss8) {   // the sum-of-squares slab as quant_mx writes it: {ss, 0, ...}
     ssq = wave_sum(ssq);
-    if (lane == 0) inv8[row] = 1.0f / (sqrtf(ssq) * rsqrtf((float)kD) + kRmsEps);
+    if (lane < kSsSlots) ss8[(int64_t)row * kSsSlots + lane] = lane == 0 ? ssq : 0.f;
   }
 }
 
 hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st,
-                          uint8_t* q8, uint8_t* s8, float* inv8) {
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, inv8);
+                          uint8_t* q8, uint8_t* s8, float* ss8) {
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8);
   return hipGetLastError();
 }
 

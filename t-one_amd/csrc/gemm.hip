@@ -249,6 +249,44 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
   }
   const bool nt = p.nt_store;
   const bool full = m0 + TL::BM <= p.M;        // block-uniform: no row guards
+  if constexpr (EPI == EPI_RESID && !SPLIT && RV == 32) {
+    if (p.C8) {
+      // fp8 mode: the shadow's MXFP8 form, as quant_mx would make it from the shadow (a 32-column block = 8 lanes),
+      // and the row's sum of squares over the tile's 128 columns into the first of its 4 slots of the slab
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int q = tid + k * NT, row = q / RV, c = (q % RV) * 4;
+        const int grow = m0 + row;
+        const bool ok = full || grow < p.M;
+        const f32x4 v = res[k] + p.alpha * val[k];
+        const int64_t o = (int64_t)grow * p.ldc + ocol0 + c;
+        u32x2 h;
+        h.x = pack_bf16x2(v.x, v.y);
+        h.y = pack_bf16x2(v.z, v.w);
+        if (ok) {
+          st_out(reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + o), v, nt);
+          if (p.C2) st_out(reinterpret_cast<u32x2*>(p.C2 + o), h, nt);
+        }
+        const float b0 = __uint_as_float(h.x << 16), b1 = __uint_as_float(h.x & 0xffff0000u);
+        const float b2 = __uint_as_float(h.y << 16), b3 = __uint_as_float(h.y & 0xffff0000u);
+        float am = fmaxf(fmaxf(fabsf(b0), fabsf(b1)), fmaxf(fabsf(b2), fabsf(b3)));
+        am = fmaxf(am, __shfl_xor(am, 1, 64));
+        am = fmaxf(am, __shfl_xor(am, 2, 64));
+        am = fmaxf(am, __shfl_xor(am, 4, 64));
+        const int e = mx_exp(am);
+        const uint32_t q4 = quant4(b0, b1, b2, b3, exp2i(e));
+        float ssq = fmaf(b3, b3, fmaf(b2, b2, fmaf(b1, b1, b0 * b0)));
+#pragma unroll
+        for (int w = 1; w < 32; w <<= 1) ssq += __shfl_xor(ssq, w, 64);
+        if (ok) {
+          *reinterpret_cast<uint32_t*>(p.C8 + o) = q4;
+          if ((q & 7) == 0) p.C8s[grow * (p.ldc / 32) + (ocol0 + c) / 32] = (uint8_t)e;
+          if ((q & 31) < 4) p.ss8[grow * kSsSlots + ocol0 / 32 + (q & 31)] = (q & 31) == 0 ? ssq : 0.f;
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int q = tid + k * NT, row = q / RV, c = (q % RV) * 4;
@@ -795,8 +833,10 @@ static hipError_t launch_glds_epi(const GemmArgs& a, int epi, int nsplit, hipStr
 }
 
 // bf16 operands already in memory: LDS-DMA kernels
-static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
+// c8_done: set when the launched kernel also wrote a RESID's MXFP8 outputs (a.C8; the LDS-DMA kernels without K split)
+static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st, bool* c8_done) {
   constexpr int kTarget = 512;
+  *c8_done = false;
   // large batches: the persistent transposed-orientation kernels (gemm_t.hip, tools/gemm_bench sweep)
   const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
   // K = 384 paired projections from 40 (SwiGLU) / 60 (GLU) blocks of 256 rows up: the X-stationary kernel
@@ -816,13 +856,14 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
   const int64_t t128 = (int64_t)((a.M + 127) / 128) * (a.N / 128);
   const int64_t t64 = (int64_t)((a.M + 63) / 64) * (a.N / 128);
   // 8 waves of 32x64 per 128x128 tile once there is a tile per CU (tools/gemm_bench sweep)
-  if (t128 >= kTarget / 2) return launch_glds_epi<Tile<128, 128, 4, 2>>(a, epi, 1, st);
+  if (t128 >= kTarget / 2) return *c8_done = true, launch_glds_epi<Tile<128, 128, 4, 2>>(a, epi, 1, st);
   // pw1 (GLU, N = 768) at config 4's per-GPU batch of 512 (M = 5120: 10.3 vs 11.1 us; M = 2560 on 64x128 tiles:
   // 8.5 vs 9.7; profiles/r02_b512_sweep.jsonl)
   if (epi == EPI_GLU && t128 >= 200) return launch_glds_epi<Tile<128, 128, 4, 2>>(a, epi, 1, st);
   if (epi == EPI_GLU && t64 >= 200) return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, 1, st);
   // half-chip M (the reduced layers at B = 2048): 64x128 LDS-DMA tiles (scripts/bf16_resid_sweep.sh)
-  if ((epi == EPI_STORE || epi == EPI_RESID) && t64 >= kTarget / 2) return launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, 1, st);
+  if ((epi == EPI_STORE || epi == EPI_RESID) && t64 >= kTarget / 2)
+    return *c8_done = true, launch_glds_epi<Tile<64, 128, 2, 2>, 2>(a, epi, 1, st);
   if ((epi == EPI_STORE || epi == EPI_RESID) && t64 < kTarget && a.N % 64 == 0 && a.ldc % 8 == 0 && a.lda % 8 == 0 &&
       !a.rpg)
     return gemm_f32t(a, epi, 2, st);   // 64x64 tiles (bf16 operands) instead of a split-K workspace round trip
@@ -836,6 +877,7 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st) {
       if (t64 * s >= kTarget) break;
     }
   }
+  *c8_done = nsplit == 1;
   if (nsplit > 1 || t64 >= kTarget / 2) return launch_glds_epi<Tile<64, 128, 2, 2>>(a, epi, nsplit, st);
   return launch_glds_epi<Tile<32, 128, 1, 2>>(a, epi, 1, st);
 }
@@ -888,7 +930,12 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   const int bk = bf16 ? 64 : 32;
   if (bf16 && a.a_bf16) {
     if (a.K % 64 != 0 || a.N % 128 != 0 || a.M <= 0 || (epi == EPI_RESID && a.c_bf16)) return hipErrorInvalidValue;
-    return gemm_bf16(a, epi, st);
+    if (a.C8 && (epi != EPI_RESID || !a.C2 || a.N != 32 * kSsSlots || a.ldc != a.N)) return hipErrorInvalidValue;
+    bool c8 = false;
+    const hipError_t e = gemm_bf16(a, epi, st, &c8);
+    // a route without the MXFP8 epilogue (K split, gemm_f32t): quantize the shadow it wrote
+    if (e == hipSuccess && a.C8 && !c8) return launch_quant_mx(a.C2, a.ldc, a.M, a.N, a.C8, a.C8s, a.ss8, st);
+    return e;
   }
   if (!bf16 && a.W3 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
     // fp32 by exact bf16 splitting (gemm_t.hip gemm_x3); tile per shape from tools/gemm_bench

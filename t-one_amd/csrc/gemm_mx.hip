@@ -63,7 +63,7 @@ __device__ __forceinline__ u32x2 quant8(const float (&v)[8], float inv) {
 // xor shuffles.  inv (optional): 1 / (||x||_2 / sqrt(K) + 1e-8), the folded RMSNorm row factor.
 __global__ void __launch_bounds__(256) quant_mx_kernel(const uint16_t* __restrict__ X, int64_t ldx, int M, int K,
                                                        uint8_t* __restrict__ Q, uint8_t* __restrict__ S,
-                                                       float* __restrict__ inv) {
+                                                       float* __restrict__ ss8) {
   const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;                                    // wave-uniform
   const uint16_t* x = X + (int64_t)row * ldx;
@@ -94,16 +94,16 @@ __global__ void __launch_bounds__(256) quant_mx_kernel(const uint16_t* __restric
       if ((c & 3) == 0) S[(int64_t)row * (K / 32) + c / 4] = (uint8_t)e;
     }
   }
-  if (inv) {
+  if (ss8) {   // the whole row's sum in slot 0, zeros in the others (common.h kSsSlots)
     ss = wave_sum(ss);
-    if (lane == 0) inv[row] = 1.0f / (sqrtf(ss) * rsqrtf((float)K) + kRmsEps);
+    if (lane < kSsSlots) ss8[(int64_t)row * kSsSlots + lane] = lane == 0 ? ss : 0.f;
   }
 }
 
-hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t* Q, uint8_t* S, float* inv,
+hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t* Q, uint8_t* S, float* ss8,
                            hipStream_t st) {
-  if (K % 32 || M <= 0 || ldx % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(quant_mx_kernel, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, M, K, Q, S, inv);
+  if (K % 32 || M <= 0 || ldx % 8 || (ss8 && K != 32 * kSsSlots)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(quant_mx_kernel, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, M, K, Q, S, ss8);
   return hipGetLastError();
 }
 
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
       v.w[q] = r < BNW ? *reinterpret_cast<const uint32_t*>(p.Ws + (int64_t)(n0 + r) * KB + 4 * c) : 0u;
     }
     v.b = (tid < BNW && p.bias) ? p.bias[n0 + tid] : 0.f;
-    v.r = (RS && tid < BMX) ? p.rs_inv[min(m0 + tid, p.M - 1)] : 1.f;
+    v.r = (RS && tid < BMX) ? mx_row_inv(p.rs_ss + (int64_t)min(m0 + tid, p.M - 1) * kSsSlots) : 1.f;
     return v;
   };
   auto side_store = [&](const Side& v) {
@@ -291,6 +291,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
           }
         }
       } else {
+        float vq[TI][4];   // RESID with Q8: the shadow's bf16 values, for its MXFP8 form
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           const int nl = wrow0 + 16 * i + 4 * lg;
@@ -312,6 +313,46 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
             const u32x2 w = {(uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16),
                              (uint32_t)__builtin_bit_cast(uint16_t, b2) | ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16)};
             if (ok) *reinterpret_cast<u32x2*>(dst + mrow * p.ldc + n0 + nl) = w;
+            vq[i][0] = (float)b0;
+            vq[i][1] = (float)b1;
+            vq[i][2] = (float)b2;
+            vq[i][3] = (float)b3;
+          }
+        }
+        if constexpr (EPI == EPI_RESID) {
+          if (p.Q8) {
+            // the MXFP8 form of this row's shadow values, as quant_mx would make it: a 32-column block is tiles
+            // 2k, 2k + 1 across the row's four lanes lg; the wave's partial sum of squares over its RW columns goes
+            // to the first of its RW / 32 slots of the row's sum-of-squares slab (zeros in the others)
+            float ssq = 0.f;
+#pragma unroll
+            for (int k = 0; k < TI / 2; ++k) {
+              float am = 0.f;
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  am = fmaxf(am, fabsf(vq[2 * k + h][r]));
+                  ssq = fmaf(vq[2 * k + h][r], vq[2 * k + h][r], ssq);
+                }
+              am = fmaxf(am, __shfl_xor(am, 16, 64));
+              am = fmaxf(am, __shfl_xor(am, 32, 64));
+              const int e = mx_exp(am);
+              const float sc = exp2i(e);
+              const int col = n0 + wrow0 + 32 * k + 4 * lg;
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const uint32_t q4 = quant4(vq[2 * k + h][0], vq[2 * k + h][1], vq[2 * k + h][2], vq[2 * k + h][3], sc);
+                if (ok) *reinterpret_cast<uint32_t*>(p.Q8 + mrow * p.ldc + col + 16 * h) = q4;
+              }
+              if (ok && lg == 0) p.Q8s[mrow * (p.ldc / 32) + (n0 + wrow0) / 32 + k] = (uint8_t)e;
+            }
+            ssq += __shfl_xor(ssq, 16, 64);
+            ssq += __shfl_xor(ssq, 32, 64);
+            if (ok && lg == 0) {
+#pragma unroll
+              for (int k = 0; k < RW / 32; ++k) p.ss8[mrow * kSsSlots + (n0 + wrow0) / 32 + k] = k == 0 ? ssq : 0.f;
+            }
           }
         }
       }
@@ -459,7 +500,7 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
 #undef TONE_MXA
   }
 #endif
-  if (a.rs_inv) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
+  if (a.rs_ss) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
   return hipGetLastError();
 }
@@ -567,7 +608,7 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           xs[mb][ks] = p.As[row * p.ldas + 4 * ks + lg];
         }
       }
-      inv[mb] = RS && !(DBG & 512) ? p.rs_inv[row] : 1.0f;
+      inv[mb] = RS && !(DBG & 512) ? mx_row_inv(p.rs_ss + row * kSsSlots) : 1.0f;
     }
 
     f32x4 acc[2][2][4];   // [buffer][mb][nb]
@@ -746,7 +787,7 @@ hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
   if (grid > need) grid = need;
 #ifdef XS8_ABLATE
   if constexpr (EPI == EPI_SWIGLU) {
-    switch (a.rs_inv ? a.dbg : 0) {
+    switch (a.rs_ss ? a.dbg : 0) {
 #define X8_D(d) case d: hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true, d>), dim3(grid), dim3(512), 0, st, a, nc); return hipGetLastError();
       X8_D(1) X8_D(2) X8_D(3) X8_D(4) X8_D(5) X8_D(8) X8_D(7) X8_D(16) X8_D(17) X8_D(32) X8_D(20) X8_D(259) X8_D(515) X8_D(771) X8_D(263) X8_D(19) X8_D(256) X8_D(512)
 #undef X8_D
@@ -754,7 +795,7 @@ hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
     }
   }
 #endif
-  if (a.rs_inv) hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true>), dim3(grid), dim3(512), 0, st, a, nc);
+  if (a.rs_ss) hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true>), dim3(grid), dim3(512), 0, st, a, nc);
   else hipLaunchKernelGGL((gemm_xs8_kernel<EPI, false>), dim3(grid), dim3(512), 0, st, a, nc);
   return hipGetLastError();
 }

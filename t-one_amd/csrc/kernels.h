@@ -43,6 +43,9 @@ struct GemmArgs {
   int64_t gstride;
   int n_out;          // EPI_LOGMEL: columns written
   uint16_t* C2;       // STORE/RESID: optional bf16 shadow of C (same ldc), feeds bf16 GEMMs
+  uint8_t* C8;        // fp8 mode, RESID with C2: also the MXFP8 form of the shadow, e4m3 [M][ldc] ...
+  uint8_t* C8s;       // ... E8M0 [M][ldc / 32] ...
+  float* ss8;         // ... and the rows' sum-of-squares slab [M][kSsSlots] (common.h)
   int order_n;        // bf16 LDS-DMA kernel: XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8) (large W)
   int nt_store;       // non-temporal epilogue stores
   int dbg;            // microbenchmark only: 1 = no epilogue, 4 = no K loop
@@ -80,7 +83,7 @@ struct MxArgs {
   int64_t ldas;
   const uint8_t* W;       // e4m3 [N][K]
   const uint8_t* Ws;      // E8M0 [N][K/32]
-  const float* rs_inv;    // folded RMSNorm: per-row factor 1/(rms + eps) (quant_mx), or nullptr
+  const float* rs_ss;     // folded RMSNorm: the rows' sum-of-squares slab [M][kSsSlots] (common.h), or nullptr
   const float* bias;      // [N] or nullptr
   void* C;                // STORE: fp32, or bf16 when c_bf16; RESID: fp32 (may alias R)
   int64_t ldc;            // elements (C, C2) / bytes (C8)
@@ -92,14 +95,18 @@ struct MxArgs {
   uint8_t* C8;            // SWIGLU: output as e4m3 [M][N/2] ...
   uint8_t* C8s;           // ... with E8M0 scales [M][N/64]
   int64_t ldc8s;
+  uint8_t* Q8;            // RESID with C2: also the MXFP8 form of the bf16 shadow, e4m3 [M][ldc] ...
+  uint8_t* Q8s;           // ... E8M0 [M][ldc / 32] ...
+  float* ss8;             // ... and the rows' sum-of-squares slab [M][kSsSlots]
   int M, N, K;
   int dbg;                // microbenchmarks only (gemm_mx.hip DBG bits); 0 in the session
 };
 hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st);
 // X-stationary MXFP8 GEMM for K = 384 (gemm_mx.hip gemm_xs8_kernel): SWIGLU (-> MXFP8 h) / STORE (bf16 out)
 hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st);
-// bf16 [M][K] (ldx elements) -> e4m3 [M][K] + E8M0 [M][K/32]; inv (optional): 1/(||row||/sqrt(K) + 1e-8)
-hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t* Q, uint8_t* S, float* inv,
+// bf16 [M][K] (ldx elements) -> e4m3 [M][K] + E8M0 [M][K/32]; ss8 (optional): the rows' sum-of-squares slab
+// [M][kSsSlots] as {ss, 0, ...} (the folded-RMSNorm row factor's input, common.h mx_row_inv)
+hipError_t launch_quant_mx(const uint16_t* X, int64_t ldx, int M, int K, uint8_t* Q, uint8_t* S, float* ss8,
                            hipStream_t st);
 // bf16 operands, fixed tile/stage variant (microbenchmarks)
 hipError_t gemm_bf16_variant(const GemmArgs& a, int epi, int variant, int nsplit, hipStream_t st);
@@ -159,10 +166,10 @@ hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, 
 
 // In-place RMSNorm over rows of 384 (norm_out, out_norm); optional bf16 shadow of the result
 // (3 split planes `plane` elements apart when plane > 0).
-// q8 / s8 / inv8 (fp8 mode, optional): also the MXFP8 form of the bf16 shadow row and its folded-RMSNorm row factor,
+// q8 / s8 / ss8 (fp8 mode, optional): also the MXFP8 form of the bf16 shadow row and its sum-of-squares slab,
 // exactly what launch_quant_mx would make from the shadow
 hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st,
-                          uint8_t* q8 = nullptr, uint8_t* s8 = nullptr, float* inv8 = nullptr);
+                          uint8_t* q8 = nullptr, uint8_t* s8 = nullptr, float* ss8 = nullptr);
 
 // Layers 14/15: xn = RMSNorm(r); kv = [cache(S rows) ; xn]; next cache (left-padded to 30) -> state.
 hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S,

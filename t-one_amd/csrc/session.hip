@@ -125,7 +125,7 @@ struct tone_session {
   void *x2, *flat, *h, *ctx, *d, *xn, *kv, *yred;   // bf16 in bf16 mode
   uint16_t *xbA, *xbB;                              // bf16 shadows of rA / rB (bf16 mode)
   uint8_t *a8 = nullptr, *a8s = nullptr, *h8 = nullptr, *h8s = nullptr;   // fp8 mode: MXFP8 GEMM inputs
-  float* inv8 = nullptr;                            // fp8 mode: folded-RMSNorm row factors of a8
+  float* ss8 = nullptr;                             // fp8 mode: sum-of-squares slab of a8's rows [rows][kSsSlots]
   float *ws, *ws_ss;
   int64_t ws_cap = 0;
 
@@ -391,7 +391,8 @@ struct Scope {
 
 int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, int64_t lda, const void* W, void* C,
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
-              float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr) {
+              float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr,
+              bool mx_out = false) {
   GemmArgs a{};   // value-initialised: every field not set below is zero
   a.A = A;
   a.lda = lda;
@@ -415,6 +416,11 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   a.a_bf16 = bf && a_bf16;
   a.c_bf16 = bf && c_bf16;
   a.C2 = bf ? c2 : nullptr;
+  if (mx_out) {   // fp8 mode, RESID: also the MXFP8 form of the shadow and its sum-of-squares slab (the next MX GEMM's A)
+    a.C8 = s->a8;
+    a.C8s = s->a8s;
+    a.ss8 = s->ss8;
+  }
   if (s->precision == TONE_PRECISION_FP32) {
     auto it = s->w3.find(W);
     a.W3 = it == s->w3.end() ? nullptr : it->second;
@@ -425,9 +431,9 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
 
 // fp8 mode: one MXFP8 GEMM (gemm_mx.hip); A8/As the e4m3 rows and their scales (K bytes / K/32 per row)
 int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8, const uint8_t* As, const MxW& w, void* C,
-            int64_t ldc, const float* bias, int M, int N, int K, int epi, const float* inv, const float* R = nullptr,
+            int64_t ldc, const float* bias, int M, int N, int K, int epi, const float* rs_ss, const float* R = nullptr,
             float alpha = 1.0f, bool c_bf16 = false, uint16_t* C2 = nullptr, uint8_t* C8 = nullptr,
-            uint8_t* C8s = nullptr) {
+            uint8_t* C8s = nullptr, bool mx_out = false) {
   MxArgs a{};
   a.A = A8;
   a.lda = K;
@@ -435,7 +441,7 @@ int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8,
   a.ldas = K / 32;
   a.W = w.q;
   a.Ws = w.s;
-  a.rs_inv = inv;
+  a.rs_ss = rs_ss;
   a.bias = bias;
   a.C = C;
   a.ldc = ldc;
@@ -447,6 +453,11 @@ int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8,
   a.C8 = C8;
   a.C8s = C8s;
   a.ldc8s = N / 64;
+  if (mx_out) {   // RESID: also the MXFP8 form of the shadow and its sum-of-squares slab (the next MX GEMM's A)
+    a.Q8 = s->a8;
+    a.Q8s = s->a8s;
+    a.ss8 = s->ss8;
+  }
   a.M = M;
   a.N = N;
   a.K = K;
@@ -488,15 +499,17 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, geo.chunk, s->w2p));
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * geo.T, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
-  // fp8 mode: the norms that feed a layer's FFN1 directly also emit its MXFP8 operand (no quant_mx launch)
+  // fp8 mode: the norms that feed a layer's FFN1 directly, FFN1's down-projection (before q|k|v) and pw2 (before FFN2)
+  // also emit the next MX GEMM's MXFP8 operand and its sum-of-squares slab (no quant_mx launch)
   // (TONE_FP8_NORMQ=0 keeps the separate quant_mx launches; the operands are bit-identical either way,
-  // tests/test_gpu_parity.py::test_fp8_norm_quant_fusion_matches_quant_mx; 0.6-1 % per step, profiles/r02_fp8_normq_ab.txt)
+  // tests/test_gpu_parity.py::test_fp8_norm_quant_fusion_matches_quant_mx; norms 0.6-1 % per step,
+  // profiles/r02_fp8_normq_ab.txt)
   const bool f8n = f8 && knobs().fp8_normq;
   bool q8_fresh = f8n;
-  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st, f8n ? s->a8 : nullptr, s->a8s, s->inv8));
+  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st, f8n ? s->a8 : nullptr, s->a8s, s->ss8));
   if (s->debug_stop == 1) {
     // the fused-vs-separate check reads the first FFN1's MXFP8 operand here: make it the separate way too
-    if (f8 && !f8n) LAUNCH("quant_mx", launch_quant_mx(shA, D, B * geo.T, D, s->a8, s->a8s, s->inv8, st));
+    if (f8 && !f8n) LAUNCH("quant_mx", launch_quant_mx(shA, D, B * geo.T, D, s->a8, s->a8s, s->ss8, st));
     return TONE_OK;
   }
   float* x = s->rA;
@@ -509,14 +522,17 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
     // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
     // up-projection's epilogue
+    // fp8 mode: q8_fresh = a8 / a8s / ss8 already hold the MXFP8 form of the current shadow xs -- made by the norm
+    // (norm_out / out_norm), or by the RESID GEMM that produced xs (FFN1 down before q|k|v, pw2 before FFN2), else
+    // by a quant_mx launch here
     auto ffn = [&](int f) -> int {
       if (f8) {
-        if (!(f == 0 && q8_fresh)) LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->inv8, st));
-        q8_fresh = false;
+        if (!q8_fresh) LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->ss8, st));
         CALL(mx_call(s, st, "gemm_ffn_up", s->a8, s->a8s, w.mx13[f], nullptr, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU,
-                     s->inv8, nullptr, 1.0f, false, nullptr, s->h8, s->h8s));
+                     s->ss8, nullptr, 1.0f, false, nullptr, s->h8, s->h8s));
+        q8_fresh = f8n && f == 0 && l < 14;   // FFN1 down emits the MXFP8 operand of layers 0-13's q|k|v
         return mx_call(s, st, "gemm_ffn_down", s->h8, s->h8s, w.mx2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, nullptr, x,
-                       0.5f, false, xs);
+                       0.5f, false, xs, nullptr, nullptr, q8_fresh);
       }
       CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[f], s->h, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
                      1.0f, true, true));
@@ -543,8 +559,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       const int N = rec ? 3 * D : D;
       // q/k/v in bf16 in bf16 mode (half the attention kernel's input bytes)
       if (f8) {
-        LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->inv8, st));
-        CALL(mx_call(s, st, "gemm_qkv", s->a8, s->a8s, w.mxqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, s->inv8, nullptr,
+        if (!q8_fresh) LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->ss8, st));
+        CALL(mx_call(s, st, "gemm_qkv", s->a8, s->a8s, w.mxqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, s->ss8, nullptr,
                      1.0f, true));
       } else {
         CALL(gemm_call(s, st, "gemm_qkv", xa, D, w.wqkv, s->qkv, N, w.bqkv, M, N, D, EPI_STORE, 1, nullptr, 1.0f, true,
@@ -587,16 +603,23 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     }
     LAUNCH("attention", launch_attention(aa, st));
     CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
+    q8_fresh = false;
     // Convolution module (conformer_blocks.py:827-830)
     CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true,
                    true));   // g in bf16 in the bf16 / fp8 modes (fp32 in fp32 mode: gemm_call drops c_bf16 there)
     LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st));
-    CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
+    // fp8 mode: pw2 also emits FFN2's MXFP8 operand
+    CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs, f8n));
+    q8_fresh = f8n;
+    if (s->debug_stop == 100 + l) {   // FFN2's MXFP8 operand: the pw2 epilogue's, or quant_mx's with the fusion off
+      if (f8 && !f8n) LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->ss8, st));
+      return TONE_OK;
+    }
     // FFN2 + norm_out (conformer_blocks.py:832-836)
     CALL(ffn(1));
     // the next layer's FFN1 reads this norm's output unless the reduction / upsampling comes in between
     q8_fresh = f8n && l != 6 && l < 14;
-    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->inv8));
+    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->ss8));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
       LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, geo.T, st));
       CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * geo.Tr, D, 4 * D,
@@ -886,7 +909,7 @@ int finalize_weights(tone_session* s) {
   if (s->precision == TONE_PRECISION_FP8) {
     CALL(dalloc(s, &s->a8, MB * (30 + kTMax) * D));            // the largest quantized input: layer 15's k/v rows
     CALL(dalloc(s, &s->a8s, MB * (30 + kTMax) * (D / 32)));
-    CALL(dalloc(s, &s->inv8, MB * (30 + kTMax)));
+    CALL(dalloc(s, &s->ss8, MB * (30 + kTMax) * kSsSlots));
     CALL(dalloc(s, &s->h8, MB * kTMax * kDff));
     CALL(dalloc(s, &s->h8s, MB * kTMax * (kDff / 32)));
   }
@@ -1089,7 +1112,7 @@ int tone_session_debug_read(tone_session* s, const char* buffer, void* host_dst,
   // fp8 mode: the MXFP8 operand of the next MX GEMM (e4m3 [M][384], E8M0 [M][12], fp32 row factors [M])
   else if (n == "a8" && s->a8) { p = s->a8; cap = MB * kTMax * kD; }
   else if (n == "a8s" && s->a8s) { p = s->a8s; cap = MB * kTMax * (kD / 32); }
-  else if (n == "inv8" && s->inv8) { p = s->inv8; cap = MB * kTMax * 4; }
+  else if (n == "ss8" && s->ss8) { p = s->ss8; cap = MB * kTMax * kSsSlots * 4; }
   else return fail(TONE_E_INVALID, "unknown debug buffer " + n);
   if ((size_t)bytes > cap) return fail(TONE_E_INVALID, "debug_read larger than the buffer");
   HIP_TRY(hipSetDevice(s->device));

@@ -125,6 +125,12 @@ __global__ void ref_mx_kernel(const float* A, const float* W, const float* bias,
   out[(int64_t)m * nout + o] = (float)v;
 }
 
+// the folded-RMSNorm row factor from the sum-of-squares slab (for the reference)
+__global__ void ss_to_inv_kernel(const float* ss8, float* inv, int M) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < M) inv[m] = mx_row_inv(ss8 + (int64_t)m * kSsSlots);
+}
+
 static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, const float* R, float* ref, float* err,
                    int M, int N, int K, int epi, int rowscale, int iters, int xs = 0) {
   // xs: 98 = the X-stationary kernel (gemm_xs8, SWIGLU only; XSNC = W tiles per item, 0 auto)
@@ -132,13 +138,15 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   auto mx = [&](const MxArgs& a) { return xs ? gemm_xs8(a, epi, xsnc, 0) : gemm_mx(a, epi, 0); };
   const int nout = epi >= 2 ? N / 2 : N;
   uint8_t *A8, *As, *W8, *Ws, *C8, *C8s;
-  float *inv, *Af, *Wf, *C, *Cf;
+  float *inv, *ss8, *Af, *Wf, *C, *Cf;
+  CK(hipMalloc(&ss8, (size_t)M * kSsSlots * 4));
   CK(hipMalloc(&A8, (size_t)M * K)); CK(hipMalloc(&As, (size_t)M * K / 32));
   CK(hipMalloc(&W8, (size_t)N * K)); CK(hipMalloc(&Ws, (size_t)N * K / 32));
   CK(hipMalloc(&inv, (size_t)M * 4)); CK(hipMalloc(&Af, (size_t)M * K * 4)); CK(hipMalloc(&Wf, (size_t)N * K * 4));
   CK(hipMalloc(&C, (size_t)M * nout * 4)); CK(hipMalloc(&Cf, (size_t)M * nout * 4));
   CK(hipMalloc(&C8, (size_t)M * nout)); CK(hipMalloc(&C8s, (size_t)M * nout / 32));
-  CK(launch_quant_mx(A, K, M, K, A8, As, rowscale ? inv : nullptr, 0));
+  CK(launch_quant_mx(A, K, M, K, A8, As, rowscale ? ss8 : nullptr, 0));
+  if (rowscale) hipLaunchKernelGGL(ss_to_inv_kernel, dim3((M + 255) / 256), dim3(256), 0, 0, ss8, inv, M);
   CK(launch_quant_mx(W, K, N, K, W8, Ws, nullptr, 0));
   hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)M * K + 255) / 256)), dim3(256), 0, 0, A8, As, Af, (int64_t)M, K);
   hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)N * K + 255) / 256)), dim3(256), 0, 0, W8, Ws, Wf, (int64_t)N, K);
@@ -152,7 +160,7 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
     CK(hipMemcpy2D(A8p, K + pad, A8, K, K, M, hipMemcpyDeviceToDevice));
   }
   MxArgs a{};
-  a.A = A8p; a.lda = K + pad; a.As = As; a.ldas = K / 32; a.W = W8; a.Ws = Ws; a.rs_inv = rowscale ? inv : nullptr;
+  a.A = A8p; a.lda = K + pad; a.As = As; a.ldas = K / 32; a.W = W8; a.Ws = Ws; a.rs_ss = rowscale ? ss8 : nullptr;
   a.bias = bias; a.C = C; a.ldc = nout; a.c_bf16 = 0; a.R = R; a.ldr = N; a.alpha = 1.f;
   a.C8 = C8; a.C8s = C8s; a.ldc8s = nout / 32; a.M = M; a.N = N; a.K = K;
   a.dbg = getenv("MXDBG") ? atoi(getenv("MXDBG")) : 0;   // gemm_mx.hip DBG bits (SWIGLU only)

@@ -402,13 +402,14 @@ pcm = [np.clip(np.round(rng.normal(0, 3000, (b, C.AUDIO_CHUNK_SAMPLES))), -32768
 out = {}
 lp = []
 for c in range(3):
-    if c == 2:   # the first FFN1 operand of chunk 2 (carried state), stopped right after the pre-encode norm
-        s.debug_stop(1)
-        s.step(torch.from_numpy(pcm[c]).to(s.dev), st)
-        m = b * 10
-        out["a8"] = s.debug_read("a8", (m, 384), np.uint8)
-        out["a8s"] = s.debug_read("a8s", (m, 12), np.uint8)
-        out["inv8"] = s.debug_read("inv8", (m,))
+    if c == 2:   # chunk 2 (carried state): the first FFN1 operand, stopped right after the pre-encode norm, and
+        m = b * 10   # layer 0's FFN2 operand, stopped right after pw2
+        for tag, stop in (("norm", 1), ("pw2", 100)):
+            s.debug_stop(stop)
+            s.step(torch.from_numpy(pcm[c]).to(s.dev), st)
+            out[tag + "_a8"] = s.debug_read("a8", (m, 384), np.uint8)
+            out[tag + "_a8s"] = s.debug_read("a8s", (m, 12), np.uint8)
+            out[tag + "_ss"] = s.debug_read("ss8", (m, 12)).sum(axis=1)
         s.debug_stop(-1)
     l, st = s.step(torch.from_numpy(pcm[c]).to(s.dev), st)
     lp.append(l.cpu().numpy())
@@ -418,11 +419,12 @@ np.savez(sys.argv[1], **out)
 
 
 def test_fp8_norm_quant_fusion_matches_quant_mx(tmp_path):
-    """fp8 mode: the RMSNorm kernels that feed a layer's FFN1 can emit its MXFP8 operand themselves
-    (TONE_FP8_NORMQ=1).  That operand must equal what the separate quant_mx launch makes from the bf16 shadow:
-    e4m3 values and E8M0 scales bit for bit, the row factor up to its summation order.  The logprobs of both
-    runs (3 stateful chunks) then stay within the fp8 bounds of each other (fp8 rounding flips amplify any
-    last-bit difference of the row factors downstream)."""
+    """fp8 mode: the RMSNorm kernels that feed a layer's FFN1, FFN1's down-projection (before q|k|v) and pw2 (before
+    FFN2) emit the next MX GEMM's MXFP8 operand themselves (TONE_FP8_NORMQ=1; the RESID epilogues of gemm_glds and
+    gemm_mx).  That operand must equal what the separate quant_mx launch makes from the bf16 shadow: e4m3 values and
+    E8M0 scales bit for bit, the row's sum of squares (slab slots added) up to its summation order.  Checked after
+    the pre-encode norm and after layer 0's pw2.  The logprobs of both runs (3 stateful chunks) then stay within the
+    fp8 bounds of each other (fp8 rounding flips amplify any last-bit difference of the row factors downstream)."""
     _gpu()
     import os
     import subprocess
@@ -434,9 +436,10 @@ def test_fp8_norm_quant_fusion_matches_quant_mx(tmp_path):
         env = dict(os.environ, TONE_FP8_NORMQ=flag)
         subprocess.run([sys.executable, "-c", _FP8_PROBE, str(f), root], env=env, check=True, timeout=240)
         res[flag] = np.load(f)
-    np.testing.assert_array_equal(res["1"]["a8"], res["0"]["a8"])
-    np.testing.assert_array_equal(res["1"]["a8s"], res["0"]["a8s"])
-    np.testing.assert_allclose(res["1"]["inv8"], res["0"]["inv8"], rtol=2e-6)
+    for tag in ("norm", "pw2"):
+        np.testing.assert_array_equal(res["1"][tag + "_a8"], res["0"][tag + "_a8"], err_msg=tag)
+        np.testing.assert_array_equal(res["1"][tag + "_a8s"], res["0"][tag + "_a8s"], err_msg=tag)
+        np.testing.assert_allclose(res["1"][tag + "_ss"], res["0"][tag + "_ss"], rtol=2e-6, err_msg=tag)
     assert_bf16_close(res["1"]["lp"], res["0"]["lp"], "fused vs separate", (FP8_MAX, FP8_P99, FP8_MARGIN), 0.99)
 
 
