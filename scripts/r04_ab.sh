@@ -1,0 +1,22 @@
+# A/B of two library builds on the large-batch legs: TONEHIP_LIB=t-one_amd/libtonehip_base.so (A) vs the tree's
+# libtonehip.so (B), alternating, one bench process per leg -> gpurun_out/r04_ab_<tag>.jsonl
+set -u
+tag=${1:-ab}
+out=gpurun_out/r04_ab_$tag.jsonl
+mkdir -p gpurun_out
+: > $out
+for rep in 1 2; do
+  for leg in "bf16 4096" "fp8 4096" "bf16 2048"; do
+    set -- $leg
+    for lib in base cur; do
+      if [ $lib = base ]; then export TONEHIP_LIB=t-one_amd/libtonehip_base.so; else unset TONEHIP_LIB; fi
+      timeout -k 10 240 python bench.py --precision $1 --batch $2 --steps 100 --warmup 3 --alt 0 --config4 0 --config5 0 \
+        --cpu-baseline-s 0 > gpurun_out/ab_leg.json 2> gpurun_out/ab_leg.err || { cat gpurun_out/ab_leg.err | tail -5; exit 1; }
+      python3 -c "
+import json,sys; d=json.load(open('gpurun_out/ab_leg.json'))
+print(json.dumps({'lib': '$lib', 'precision': '$1', 'batch': $2, 'rep': $rep, 'ms_per_step': d['ms_per_step'], 'value': d['value']}))" >> $out
+      tail -1 $out
+    done
+  done
+done
+unset TONEHIP_LIB

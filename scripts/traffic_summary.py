@@ -10,7 +10,7 @@ root, prec, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
 UP = {  # SWIGLU instantiations: EPI_SWIGLU = 2
     "fp32": r"gemm_x3_kernel<tone::XT<[^>]*>, 2,",
     "fp32-mfma": r"gemm_kernel<tone::Tile<[^>]*>, 2,",
-    "bf16": r"(gemm_t_kernel<tone::TT<[^>]*>, 2,|gemm_xs\d?_kernel<2, )",
+    "bf16": r"(gemm_t_kernel<tone::TT<[^>]*>, 2,|gemm_x[sw]\d?_kernel<2, )",
     "fp8": r"(gemm_xs8_kernel<2, |gemm_mx_kernel<\d+, 2, )",
 }[prec]
 # EPI_RESID = 1, in any GEMM kernel family

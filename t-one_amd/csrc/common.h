@@ -235,4 +235,38 @@ __device__ __forceinline__ void store_shadow(uint16_t* s, int64_t plane, int64_t
   store_bf16(s, i + 2 * plane, t2);
 }
 
+// The residual stream: fp32 in fp32 mode, fp16 in the bf16 / fp8 modes (as the reference's exported graph keeps it,
+// tone/scripts/export.py:411).  Element i, and four consecutive elements (16 / 8-byte aligned),
+// with the type fixed at compile time (R16) or chosen per launch (r16, the GEMM epilogues).
+template <bool R16>
+__device__ __forceinline__ float load_res(const void* base, int64_t i) {
+  if constexpr (R16) return __half2float(static_cast<const __half*>(base)[i]);
+  else return static_cast<const float*>(base)[i];
+}
+template <bool R16>
+__device__ __forceinline__ void store_res(void* base, int64_t i, float v) {
+  if constexpr (R16) static_cast<__half*>(base)[i] = __float2half_rn(v);
+  else static_cast<float*>(base)[i] = v;
+}
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4_t load_res4(const void* base, int64_t i, bool r16) {
+  if (r16) {
+    const f16x4_t h = *reinterpret_cast<const f16x4_t*>(static_cast<const __half*>(base) + i);
+    return __builtin_convertvector(h, f32x4_t);
+  }
+  return *reinterpret_cast<const f32x4_t*>(static_cast<const float*>(base) + i);
+}
+__device__ __forceinline__ void store_res4(void* base, int64_t i, f32x4_t v, bool r16, bool nt = false) {
+  if (r16) {
+    const f16x4_t h = __builtin_convertvector(v, f16x4_t);   // round to nearest even, as __float2half_rn
+    f16x4_t* d = reinterpret_cast<f16x4_t*>(static_cast<__half*>(base) + i);
+    if (nt) __builtin_nontemporal_store(h, d);
+    else *d = h;
+    return;
+  }
+  f32x4_t* d = reinterpret_cast<f32x4_t*>(static_cast<float*>(base) + i);
+  if (nt) __builtin_nontemporal_store(v, d);
+  else *d = v;
+}
+
 }  // namespace tone

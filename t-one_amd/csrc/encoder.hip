@@ -10,20 +10,22 @@ namespace tone {
 constexpr float kInvSqrtD = 0.05103103630798288f;   // 384^-0.5 (submodules.py:51)
 
 // ---------------------------------------------------------------------------------------------
-// RMSNorm (submodules.py:34-54) in place over rows of 384: one wave per row, 6 elements per lane.
-__global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, const float* __restrict__ w, int rows,
+// RMSNorm (submodules.py:34-54) in place over rows of 384: one wave per row, 6 elements per lane; the residual
+// stream x fp32, or fp16 in the bf16 / fp8 modes (R16).
+template <bool R16>
+__global__ void __launch_bounds__(256) rmsnorm_kernel(void* __restrict__ x, const float* __restrict__ w, int rows,
                                                       uint16_t* __restrict__ shadow, int64_t plane,
                                                       uint8_t* __restrict__ q8, uint8_t* __restrict__ s8,
                                                       float* __restrict__ ss8) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  float* xr = x + (int64_t)row * kD;
+  const int64_t xr = (int64_t)row * kD;
   float v[6];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    v[i] = xr[lane + 64 * i];
+    v[i] = load_res<R16>(x, xr + lane + 64 * i);
     ss += v[i] * v[i];
   }
   ss = wave_sum(ss);
@@ -32,7 +34,7 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, con
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const float y = w[lane + 64 * i] * (v[i] / den);
-    xr[lane + 64 * i] = y;
+    store_res<R16>(x, xr + lane + 64 * i, y);
     if (shadow) store_shadow(shadow, plane, (int64_t)row * kD + lane + 64 * i, y);
     if (q8) {
       // fp8 mode: the MXFP8 form of the bf16 shadow row for the next layer's FFN up-projection, as
@@ -55,9 +57,12 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(float* __restrict__ x, con
   }
 }
 
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st,
+hipError_t launch_rmsnorm(void* x, const float* w, int rows, uint16_t* shadow, int64_t plane, bool r16, hipStream_t st,
                           uint8_t* q8, uint8_t* s8, float* ss8) {
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8);
+  if (r16)
+    hipLaunchKernelGGL(rmsnorm_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8);
   return hipGetLastError();
 }
 
@@ -67,7 +72,7 @@ hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, 
 // kv = [cache_S ; xn] and keeps [cache_S[T:] ; xn] (submodules.py:295-302); update_after_layer
 // left-pads it with zeros to 30 rows (conformer_blocks.py:161-163).  xn = norm_self_att(r).
 template <bool OBF>
-__global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restrict__ r, const float* __restrict__ norm_w,
+__global__ void __launch_bounds__(256) kv_assemble_kernel(const void* __restrict__ r, const float* __restrict__ norm_w,
                                                           StateRef s, int layer_slot, int T, int S,
                                                           void* __restrict__ xn, void* __restrict__ kv) {
   // grid (B, ns): workgroup y takes rows 4y..4y+3 and every ns-th 256-element block of the state
@@ -79,10 +84,10 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
   const int TK = S + T;
   // normalized current rows
   for (int i = 4 * y + wid; i < T; i += 4 * ns) {
-    const float* xr = r + ((int64_t)b * T + i) * kD;
+    const int64_t xr = ((int64_t)b * T + i) * kD;   // the residual stream: fp16 in the bf16 / fp8 modes (OBF)
     float v[6], ss = 0.f;
 #pragma unroll
-    for (int e = 0; e < 6; ++e) { v[e] = xr[lane + 64 * e]; ss += v[e] * v[e]; }
+    for (int e = 0; e < 6; ++e) { v[e] = load_res<OBF>(r, xr + lane + 64 * e); ss += v[e] * v[e]; }
     ss = wave_sum(ss);
     const float den = sqrtf(ss) * kInvSqrtD + kRmsEps;
 #pragma unroll
@@ -109,7 +114,7 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const float* __restric
   }
 }
 
-hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S, void* xn,
+hipError_t launch_kv_assemble(const void* r, const float* norm_w, StateRef s, int layer_slot, int T, int S, void* xn,
                               void* kv, bool obf, int B, hipStream_t st) {
   const dim3 grid(B, B >= 1024 ? 1 : 4);
   if (obf) hipLaunchKernelGGL(kv_assemble_kernel<true>, grid, dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
@@ -402,7 +407,7 @@ hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, c
 //   y[o][t] = bias[o] + sum_{k<3} w[o][k] x[o/4][2t+k], o < 1536, t < Tr = (T + 1 - 3) / 2 + 1
 //   (no padding in the streaming branch: T = 13 gives Tr = 6 and leaves the last frame to the state)
 template <bool OBF, int T>
-__global__ void __launch_bounds__(256) reduce_conv_kernel(const float* __restrict__ x, StateRef s,
+__global__ void __launch_bounds__(256) reduce_conv_kernel(const void* __restrict__ x, StateRef s,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           void* __restrict__ y, int B) {
   constexpr int TR = (T + 1 - 3) / 2 + 1;
@@ -411,7 +416,7 @@ __global__ void __launch_bounds__(256) reduce_conv_kernel(const float* __restric
   const int b = idx / kD, c = idx % kD;
   float xc[T + 1];
   xc[0] = __half2float(s.in[s.row_in(b) + kOffRed + c]);
-  for (int t = 0; t < T; ++t) xc[t + 1] = x[((int64_t)b * T + t) * kD + c];
+  for (int t = 0; t < T; ++t) xc[t + 1] = load_res<OBF>(x, ((int64_t)b * T + t) * kD + c);   // fp16 residual when OBF
   s.out[s.row_out(b) + kOffRed + c] = __float2half_rn(xc[T]);
   for (int q = 0; q < 4; ++q) {
     const int o = 4 * c + q;
@@ -421,7 +426,7 @@ __global__ void __launch_bounds__(256) reduce_conv_kernel(const float* __restric
   }
 }
 
-hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
+hipError_t launch_reduce_conv(const void* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
                               int T, hipStream_t st) {
   const dim3 grid((B * kD + 255) / 256), block(256);
   if (T == kT && obf) hipLaunchKernelGGL((reduce_conv_kernel<true, kT>), grid, block, 0, st, x, s, w, b, y, B);
@@ -436,23 +441,29 @@ hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const 
 // TemporalUpsampling (conformer_blocks.py:955-988): repeat_interleave x2, right-pad 1, trim to T, + residual.
 // Frames t < 2 Tr take x5[t / 2]; a frame past 2 Tr (t = 12 of a 400 ms chunk: 2 x 6 < 13) is the zero pad,
 // so it keeps the residual alone.
-__global__ void __launch_bounds__(256) upsample_add_kernel(float* __restrict__ x10, const float* __restrict__ x5, int B,
+template <bool R16>
+__global__ void __launch_bounds__(256) upsample_add_kernel(void* __restrict__ x10, const void* __restrict__ x5, int B,
                                                            int T, int Tr, uint16_t* __restrict__ shadow, int64_t plane) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)B * T * kD) return;
   const int64_t row = idx / kD;
   const int c = idx % kD;
   const int64_t b = row / T, t = row % T;
-  const float v = (t < 2 * Tr ? x5[(b * Tr + t / 2) * kD + c] : 0.0f) + x10[idx];
-  x10[idx] = v;
+  const float v = (t < 2 * Tr ? load_res<R16>(x5, (b * Tr + t / 2) * kD + c) : 0.0f) + load_res<R16>(x10, idx);
+  store_res<R16>(x10, idx, v);
   if (shadow) store_shadow(shadow, plane, idx, v);
 }
 
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, int T, uint16_t* shadow, int64_t plane, hipStream_t st) {
+hipError_t launch_upsample_add(void* x10, const void* x5, int B, int T, uint16_t* shadow, int64_t plane, bool r16,
+                               hipStream_t st) {
   const int64_t n = (int64_t)B * T * kD;
   const int Tr = (T + 1 - 3) / 2 + 1;
-  hipLaunchKernelGGL(upsample_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr, shadow,
-                     plane);
+  if (r16)
+    hipLaunchKernelGGL(upsample_add_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
+                       shadow, plane);
+  else
+    hipLaunchKernelGGL(upsample_add_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
+                       shadow, plane);
   return hipGetLastError();
 }
 
@@ -467,7 +478,8 @@ hipError_t launch_upsample_add(float* x10, const float* x5, int B, int T, uint16
 constexpr float kSilenceThreshold = 0.9f;
 constexpr int kHeadQ = kD / 4;              // 96
 constexpr int kHeadWs = kHeadQ + 4;         // padded LDS row of a W quarter (bank spread)
-__global__ void __launch_bounds__(256) head_kernel(const float* __restrict__ x, const float* __restrict__ w,
+template <bool R16>
+__global__ void __launch_bounds__(256) head_kernel(const void* __restrict__ x, const float* __restrict__ w,
                                                    const float* __restrict__ bias, float* __restrict__ logp,
                                                    int32_t* __restrict__ frame_info, int rows) {
   __shared__ __attribute__((aligned(16))) float ws[4 * kVocab * kHeadWs];   // [quarter][v][96 (+4)]
@@ -478,13 +490,13 @@ __global__ void __launch_bounds__(256) head_kernel(const float* __restrict__ x, 
   }
   __syncthreads();
   const int row = blockIdx.x * 64 + (tid >> 2), q = lane & 3;
-  const float* xr = x + (int64_t)min(row, rows - 1) * kD + q * kHeadQ;
+  const int64_t xr = (int64_t)min(row, rows - 1) * kD + q * kHeadQ;   // the residual stream (fp16 when R16)
   const float* wq = ws + q * kVocab * kHeadWs;
   float acc[kVocab];
 #pragma unroll
   for (int v = 0; v < kVocab; ++v) acc[v] = 0.f;
   for (int k = 0; k < kHeadQ; k += 4) {
-    const f32x4_t xv = *reinterpret_cast<const f32x4_t*>(xr + k);
+    const f32x4_t xv = load_res4(x, xr + k, R16);
 #pragma unroll
     for (int v = 0; v < kVocab; ++v) {
       const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(wq + v * kHeadWs + k);
@@ -528,15 +540,16 @@ __global__ void __launch_bounds__(256) head_kernel(const float* __restrict__ x, 
 // The same for a few rows (the drop-in's B = 1 .. 6 streams): one wave per row, lane l owns k = l + 64 i (six k), W
 // read straight from L2 (no LDS staging, which the 256-row blocks amortise), the 35 partial sums combined by a
 // six-step xor butterfly; then the same log-softmax / greedy / speech-flag epilogue.
-__global__ void __launch_bounds__(256) head_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
+template <bool R16>
+__global__ void __launch_bounds__(256) head_rows_kernel(const void* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, float* __restrict__ logp,
                                                         int32_t* __restrict__ frame_info, int rows) {
   const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;                                       // wave-uniform
-  const float* xr = x + (int64_t)row * kD;
+  const int64_t xr = (int64_t)row * kD;
   float xv[kD / 64];
 #pragma unroll
-  for (int i = 0; i < kD / 64; ++i) xv[i] = xr[lane + 64 * i];
+  for (int i = 0; i < kD / 64; ++i) xv[i] = load_res<R16>(x, xr + lane + 64 * i);
   float acc[kVocab];
 #pragma unroll
   for (int v = 0; v < kVocab; ++v) {
@@ -570,14 +583,16 @@ __global__ void __launch_bounds__(256) head_rows_kernel(const float* __restrict_
   }
 }
 
-hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows,
+hipError_t launch_head(const void* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows, bool r16,
                        hipStream_t st) {
   if (rows <= 0) return hipSuccess;
   if (rows <= 64) {
-    hipLaunchKernelGGL(head_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
+    if (r16) hipLaunchKernelGGL(head_rows_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
+    else hipLaunchKernelGGL(head_rows_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(head_kernel, dim3((rows + 63) / 64), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
+  if (r16) hipLaunchKernelGGL(head_kernel<true>, dim3((rows + 63) / 64), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
+  else hipLaunchKernelGGL(head_kernel<false>, dim3((rows + 63) / 64), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
   return hipGetLastError();
 }
 

@@ -81,7 +81,10 @@ struct Tile {
 // Every operand the epilogue reads (bias, BN scale/shift, residual rows) is loaded into registers
 // before the first store: C may alias R, so a load placed after a store could not be hoisted and
 // each one would pay a full memory latency in series.
-template <class TL, int EPI, bool CBF, bool SPLIT, int TM = TL::BM / TL::WM / 32, int TN = TL::BN / TL::WN / 32>
+// R16: the residual stream R / C (RESID, and a STORE that starts it) is fp16 (bf16 / fp8 modes), a compile-time choice so
+// the residual loads stay straight-line (a per-launch branch makes the compiler drain them one at a time)
+template <class TL, int EPI, bool CBF, bool SPLIT, bool R16 = false, int TM = TL::BM / TL::WM / 32,
+          int TN = TL::BN / TL::WN / 32>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[TM][TN], const float* rden, int m0, int n0,
                                               int wm, int wn, int lane) {
   constexpr int WTM = TL::BM / TL::WM, WTN = TL::BN / TL::WN;
@@ -108,7 +111,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[T
       for (int r = 0; r < 16; ++r) {
         const int row = min(m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, p.M - 1);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) rres[r][j] = p.R[(int64_t)row * p.ldr + cbase + j * 32];
+        for (int j = 0; j < TN; ++j) {
+          const int64_t o = (int64_t)row * p.ldr + cbase + j * 32;
+          rres[r][j] = R16 ? __half2float(reinterpret_cast<const __half*>(p.R)[o]) : p.R[o];
+        }
       }
     }
 #pragma unroll
@@ -146,6 +152,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, f32x16 (&acc)[T
           v += bcol[j];
           if constexpr (EPI == EPI_RESID) v = rres[r][j] + p.alpha * v;
           if constexpr (CBF) st_out(static_cast<uint16_t*>(p.C) + (int64_t)row * p.ldc + col, bf16_bits(v), nt);
+          else if (R16) static_cast<__half*>(p.C)[(int64_t)row * p.ldc + col] = __float2half_rn(v);   // fp16 residual
           else st_out(static_cast<float*>(p.C) + (int64_t)row * p.ldc + col, v, nt);
           if (p.C2) st_out(p.C2 + (int64_t)row * p.ldc + col, bf16_bits(v), nt);   // bf16 shadow of the residual
         }
@@ -189,9 +196,11 @@ __device__ __forceinline__ void wait_vmcnt() {
 // stage buffers are free after the K loop), then the block writes whole output rows with 16-byte
 // fp32 / 8-byte bf16 vectors, so each 128-byte line leaves in one instruction instead of as 64-byte
 // halves from two waves, and residual rows are read as vectors (all before the first store).
-template <class TL, int EPI, bool CBF, bool SPLIT, int TM, int TN>
+// PRE (RESID): the residual rows were loaded by the caller before its K loop (rin, in the order below), so their
+// latency hides under the MFMAs instead of stalling the epilogue
+template <class TL, int EPI, bool CBF, bool SPLIT, bool R16, bool PRE = false, int TM, int TN, int NVR = 1>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&acc)[TM][TN], const float* rden, float* Cs,
-                                                  int m0, int n0, int wm, int wn, int tid) {
+                                                  int m0, int n0, int wm, int wn, int tid, const f32x4 (&rin)[NVR] = {}) {
   constexpr int NT = TL::WM * TL::WN * 64;
   constexpr int WTM = TL::BM / TL::WM, WTN = TL::BN / TL::WN;
   constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
@@ -243,8 +252,13 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
     const int q = tid + k * NT, row = q / RV, c = (q % RV) * 4;
     val[k] = *reinterpret_cast<const f32x4*>(Cs + row * BNO + c);
     if constexpr (EPI == EPI_RESID && !SPLIT) {
-      const int grow = min(m0 + row, p.M - 1);
-      res[k] = *reinterpret_cast<const f32x4*>(p.R + (int64_t)grow * p.ldr + ocol0 + c);
+      if constexpr (PRE) {
+        static_assert(NVR == NV, "prefetched residual vectors");
+        res[k] = rin[k];
+      } else {
+        const int grow = min(m0 + row, p.M - 1);
+        res[k] = load_res4(p.R, (int64_t)grow * p.ldr + ocol0 + c, R16);
+      }
     }
   }
   const bool nt = p.nt_store;
@@ -264,7 +278,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
         h.x = pack_bf16x2(v.x, v.y);
         h.y = pack_bf16x2(v.z, v.w);
         if (ok) {
-          st_out(reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + o), v, nt);
+          store_res4(p.C, o, v, R16, nt);
           if (p.C2) st_out(reinterpret_cast<u32x2*>(p.C2 + o), h, nt);
         }
         const float b0 = __uint_as_float(h.x << 16), b1 = __uint_as_float(h.x & 0xffff0000u);
@@ -303,7 +317,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
     h.x = pack_bf16x2(v.x, v.y);
     h.y = pack_bf16x2(v.z, v.w);
     if constexpr (CBF) st_out(reinterpret_cast<u32x2*>(static_cast<uint16_t*>(p.C) + o), h, nt);
-    else st_out(reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + o), v, nt);
+    else store_res4(p.C, o, v, R16, nt);   // fp32, or the fp16 residual stream (R16)
     if (p.C2) st_out(reinterpret_cast<u32x2*>(p.C2 + o), h, nt);
   }
 }
@@ -512,7 +526,7 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
   constexpr bool kLdsEpi = (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU || EPI == EPI_GLU) &&
                            BM * BN * 4 <= (int)sizeof(lds_all);
   if constexpr (kLdsEpi) {
-    gemm_epilogue_lds<TL, EPI, CBF, SPLIT>(p, acc, rden, reinterpret_cast<float*>(lds_all), m0, n0, wm, wn, tid);
+    gemm_epilogue_lds<TL, EPI, CBF, SPLIT, false>(p, acc, rden, reinterpret_cast<float*>(lds_all), m0, n0, wm, wn, tid);
   } else {
     gemm_epilogue<TL, EPI, CBF, SPLIT>(p, acc, rden, m0, n0, wm, wn, lane);
   }
@@ -529,7 +543,7 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
 // its own A fragments (waves of the first N column only).
 // Split-K is a runtime mode here (p.k_split > 0: K slice blockIdx.y, raw partials to p.ws).
 
-template <class TL, int EPI, bool CBF, int S>
+template <class TL, int EPI, bool CBF, int S, bool R16 = false>
 __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArgs p) {
   constexpr int BM = TL::BM, BN = TL::BN, WM = TL::WM, WN = TL::WN;
   constexpr int kNWaves = WM * WN;
@@ -620,6 +634,24 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
     }
   };
 
+  // RESID through the LDS epilogue: this tile's residual rows (the epilogue's vector order) requested before the K
+  // loop, in their stored type (converted after it), so their latency hides under the MFMAs (the epilogue would
+  // otherwise wait a full memory round trip with the matrix pipe idle); C may alias R, and only this tile writes it
+  constexpr bool kLdsEpiC = (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU || EPI == EPI_GLU) &&
+                            BM * BN * 4 <= S * kStageElems * 2;
+  constexpr bool kPre = kLdsEpiC && EPI == EPI_RESID;
+  constexpr int kRV = BN / 4, kNVR = kPre ? BM * kRV / (kNWaves * 64) : 1;
+  using RawT = typename std::conditional<R16, f16x4_t, f32x4>::type;
+  RawT rraw[kNVR];
+  if constexpr (kPre) {
+#pragma unroll
+    for (int k = 0; k < kNVR; ++k) {
+      const int q = tid + k * kNWaves * 64, row = q / kRV, c = (q % kRV) * 4;
+      const int grow = min(m0 + row, p.M - 1);
+      rraw[k] = *reinterpret_cast<const RawT*>(static_cast<const char*>(static_cast<const void*>(p.R)) +
+                                              ((int64_t)grow * p.ldr + n0 + c) * (R16 ? 2 : 4));
+    }
+  }
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -707,11 +739,21 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
     float* Cs = reinterpret_cast<float*>(lds);
     if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
       if (split) {
-        gemm_epilogue_lds<TL, EPI_STORE, false, true>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
+        gemm_epilogue_lds<TL, EPI_STORE, false, true, false>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
         return;
       }
     }
-    gemm_epilogue_lds<TL, EPI, CBF, false>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
+    if constexpr (kPre) {
+      f32x4 rin[kNVR];
+#pragma unroll
+      for (int k = 0; k < kNVR; ++k) {
+        if constexpr (R16) rin[k] = __builtin_convertvector(rraw[k], f32x4);
+        else rin[k] = rraw[k];
+      }
+      gemm_epilogue_lds<TL, EPI, CBF, false, R16, true>(p, acc, rden, Cs, m0, n0, wm, wn, tid, rin);
+    } else {
+      gemm_epilogue_lds<TL, EPI, CBF, false, R16>(p, acc, rden, Cs, m0, n0, wm, wn, tid);
+    }
     return;
   }
   if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
@@ -720,7 +762,7 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
       return;
     }
   }
-  gemm_epilogue<TL, EPI, CBF, false>(p, acc, rden, m0, n0, wm, wn, lane);
+  gemm_epilogue<TL, EPI, CBF, false, R16>(p, acc, rden, m0, n0, wm, wn, lane);
 }
 
 // Split-K combine: fixed-order sum of the partials, then the STORE/RESID epilogue.
@@ -740,12 +782,21 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmArgs p, int ns
   }
   if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + col);
   if constexpr (EPI == EPI_RESID) {
-    const float* r = p.R + (int64_t)row * p.ldr + col;
-    v.x = r[0] + p.alpha * v.x; v.y = r[1] + p.alpha * v.y; v.z = r[2] + p.alpha * v.z; v.w = r[3] + p.alpha * v.w;
+    if (p.res16) {
+      const __half* r = reinterpret_cast<const __half*>(p.R) + (int64_t)row * p.ldr + col;
+      v.x = __half2float(r[0]) + p.alpha * v.x; v.y = __half2float(r[1]) + p.alpha * v.y;
+      v.z = __half2float(r[2]) + p.alpha * v.z; v.w = __half2float(r[3]) + p.alpha * v.w;
+    } else {
+      const float* r = p.R + (int64_t)row * p.ldr + col;
+      v.x = r[0] + p.alpha * v.x; v.y = r[1] + p.alpha * v.y; v.z = r[2] + p.alpha * v.z; v.w = r[3] + p.alpha * v.w;
+    }
   }
   if constexpr (CBF) {
     uint16_t* d = static_cast<uint16_t*>(p.C) + (int64_t)row * p.ldc + col;
     d[0] = bf16_bits(v.x); d[1] = bf16_bits(v.y); d[2] = bf16_bits(v.z); d[3] = bf16_bits(v.w);
+  } else if (p.res16) {
+    __half* d = static_cast<__half*>(p.C) + (int64_t)row * p.ldc + col;
+    d[0] = __float2half_rn(v.x); d[1] = __float2half_rn(v.y); d[2] = __float2half_rn(v.z); d[3] = __float2half_rn(v.w);
   } else {
     float* d = static_cast<float*>(p.C) + (int64_t)row * p.ldc + col;
     d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
@@ -817,6 +868,12 @@ static hipError_t launch_glds(const GemmArgs& a, int nsplit, hipStream_t st) {
   }
   GemmArgs c = a;
   c.k_split = 0;
+  if constexpr ((EPI == EPI_STORE || EPI == EPI_RESID) && !CBF) {
+    if (c.res16) {
+      hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI, CBF, S, true>), dim3(tiles), block, 0, st, c);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((gemm_glds_kernel<TL, EPI, CBF, S>), dim3(tiles), block, 0, st, c);
   return hipGetLastError();
 }
@@ -928,6 +985,8 @@ hipError_t gemm_x3_splitk(const GemmArgs& a, int epi, int variant, int nsplit, h
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   const int bk = bf16 ? 64 : 32;
+  // the fp16 residual stream exists in the bf16 / fp8 modes only (the LDS-DMA and f32t kernels of gemm_bf16)
+  if (a.res16 && (!bf16 || !a.a_bf16 || a.c_bf16 || (epi != EPI_STORE && epi != EPI_RESID))) return hipErrorInvalidValue;
   if (bf16 && a.a_bf16) {
     if (a.K % 64 != 0 || a.N % 128 != 0 || a.M <= 0 || (epi == EPI_RESID && a.c_bf16)) return hipErrorInvalidValue;
     if (a.C8 && (epi != EPI_RESID || !a.C2 || a.N != 32 * kSsSlots || a.ldc != a.N)) return hipErrorInvalidValue;

@@ -84,7 +84,8 @@ __device__ __forceinline__ void store_tile_split(uint16_t* rowp, int64_t plane, 
 // m-tile j); rd[m - m0] the row-scale denominators, sb[n - n0] the bias (both LDS).
 // tile_epilogue_inv: the same with the row factors 1 / rden of this lane's rows (row wm * WTM + 32 j + lr)
 // already in registers.
-template <int EPI, bool RS, int TI, int TJ, int WTN, int WTM>
+// R16: the residual stream R / C is fp16 (bf16 / fp8 modes; compile-time, see gemm.hip gemm_epilogue)
+template <int EPI, bool RS, int TI, int TJ, int WTN, int WTM, bool R16 = false>
 __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&acc)[TI][TJ], const float (&invj)[TJ],
                                                   const float* sb, int m0, int n0, int wn, int wm, int lr, int lh) {
   constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
@@ -150,7 +151,7 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
         if constexpr (EPI == EPI_RESID) {
           f32x4 rr[4];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) rr[g] = *reinterpret_cast<const f32x4*>(p.R + mrow * p.ldr + nb + 8 * g + 4 * lh);
+          for (int g = 0; g < 4; ++g) rr[g] = load_res4(p.R, mrow * p.ldr + nb + 8 * g + 4 * lh, R16);
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             f32x4 o;
@@ -159,7 +160,7 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
             o.z = rr[g].z + p.alpha * v[4 * g + 2];
             o.w = rr[g].w + p.alpha * v[4 * g + 3];
             v[4 * g] = o.x; v[4 * g + 1] = o.y; v[4 * g + 2] = o.z; v[4 * g + 3] = o.w;
-            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
+            if (ok) store_res4(p.C, mrow * p.ldc + nb + 8 * g + 4 * lh, o, R16);
           }
           if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
           else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);
@@ -169,7 +170,7 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const f32x4 o = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
-            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + nb + 8 * g + 4 * lh) = o;
+            if (ok) store_res4(p.C, mrow * p.ldc + nb + 8 * g + 4 * lh, o, R16);   // fp32 or fp16 residual
           }
           if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
           else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);   // bf16 shadow (fp32 C)
@@ -179,13 +180,13 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
   }
 }
 
-template <int EPI, bool RS, int TI, int TJ, int WTN, int WTM>
+template <int EPI, bool RS, int TI, int TJ, int WTN, int WTM, bool R16 = false>
 __device__ __forceinline__ void tile_epilogue(const GemmArgs& p, f32x16 (&acc)[TI][TJ], const float* rd, const float* sb,
                                               int m0, int n0, int wn, int wm, int lr, int lh) {
   float invj[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) invj[j] = RS ? 1.0f / rd[wm * WTM + 32 * j + lr] : 1.0f;
-  tile_epilogue_inv<EPI, RS, TI, TJ, WTN, WTM>(p, acc, invj, sb, m0, n0, wn, wm, lr, lh);
+  tile_epilogue_inv<EPI, RS, TI, TJ, WTN, WTM, R16>(p, acc, invj, sb, m0, n0, wn, wm, lr, lh);
 }
 
 

@@ -119,7 +119,7 @@ __device__ __forceinline__ int mx_swz(int r) { return (r >> 1) & 7; }
 // loaded for the first tile only, bit 2 no MFMA; every accumulator stays live
 // BMX: X rows per tile (256, or 128 for STORE / RESID when the 256-row tiles would leave the CUs one tile each:
 // two tiles per CU overlap one tile's HBM-bound epilogue with the next one's K loop); waves WNW (W) x WMW (X)
-template <int BNW, int EPI, bool RS, int DBG = 0, int BMX = 256>
+template <int BNW, int EPI, bool RS, int DBG = 0, int BMX = 256, bool R16 = false>
 __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
   constexpr int BK = 128, QB = 128 * BK, NQW = BNW / 128, XQ = BMX / 128, STG = (NQW + XQ) * QB;
   constexpr int WMW = BMX / 64, WNW = 8 / WMW, RW = BNW / WNW;   // waves along X / W, W rows per wave
@@ -299,13 +299,13 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[i][j][r], inv, sb[nl + r]);
           if constexpr (EPI == EPI_RESID) {
-            const f32x4 rr = *reinterpret_cast<const f32x4*>(p.R + mrow * p.ldr + n0 + nl);
+            const f32x4 rr = load_res4(p.R, mrow * p.ldr + n0 + nl, R16);   // fp32 or the fp16 residual stream
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = rr[r] + p.alpha * v[r];
           }
           if (EPI == EPI_RESID || !p.c_bf16) {
             const f32x4 w = {v[0], v[1], v[2], v[3]};
-            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + n0 + nl) = w;
+            if (ok) store_res4(p.C, mrow * p.ldc + n0 + nl, w, EPI == EPI_RESID && R16);
           }
           if ((EPI == EPI_STORE && p.c_bf16) || p.C2) {
             uint16_t* dst = (EPI == EPI_STORE && p.c_bf16) ? static_cast<uint16_t*>(p.C) : p.C2;
@@ -500,6 +500,13 @@ hipError_t launch_mx(const MxArgs& a, hipStream_t st) {
 #undef TONE_MXA
   }
 #endif
+  if constexpr (EPI == EPI_RESID) {   // the residual stream fp16 (R16, the fp8 mode's) or fp32
+    if (a.rs_ss) return hipErrorInvalidValue;
+    if (a.res16) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 0, BMX, true>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
+    return hipGetLastError();
+  }
+  if (a.res16) return hipErrorInvalidValue;
   if (a.rs_ss) hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, true, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((gemm_mx_kernel<BNW, EPI, false, 0, BMX>), dim3(grid), dim3(512), 0, st, a);
   return hipGetLastError();

@@ -307,7 +307,7 @@ struct FT {
   static constexpr int BNW = BNW_, BMX = BMX_, WN = WN_, WM = WM_, WK = WK_;
 };
 
-template <class TL, int EPI, bool RS, bool BF>
+template <class TL, int EPI, bool RS, bool BF, bool R16 = false>
 __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kernel(GemmArgs p) {
   constexpr int BNW = TL::BNW, BMX = TL::BMX, WN = TL::WN, WM = TL::WM, WK = TL::WK;
   constexpr int NW = WN * WM * WK, NT = NW * 64, S = 3;
@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kerne
     if (wk == 0 && wn < TJ && lh == 0) rden[wm * WTM + 32 * jss + lr] = sqrtf(t) * p.inv_sqrt_k + kRmsEps;
     barrier_lds();
   }
-  if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
+  if (wk == 0) tile_epilogue<EPI, RS, TI, TJ, WTN, WTM, R16>(p, acc, rden, sbias, m0, n0, wn, wm, lr, lh);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1136,6 +1136,14 @@ hipError_t launch_f32t(const GemmArgs& a, hipStream_t st) {
   if (a.N % TL::BNW || a.K % (kg * TL::WK) || a.rpg || a.M <= 0 || (a.ldc % 8) || (a.lda % 8)) return hipErrorInvalidValue;
   const int tiles = (a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
+  if (a.res16) {   // the bf16 / fp8 modes' fp16 residual stream: RESID, or the STORE that starts it
+    if constexpr (BF && (EPI == EPI_STORE || EPI == EPI_RESID)) {
+      if (a.rowscale || a.c_bf16) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, false, BF, true>), dim3(tiles), block, 0, st, a);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (a.rowscale) hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, true, BF>), dim3(tiles), block, 0, st, a);
   else hipLaunchKernelGGL((gemm_f32t_kernel<TL, EPI, false, BF>), dim3(tiles), block, 0, st, a);
   return hipGetLastError();

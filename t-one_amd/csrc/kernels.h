@@ -56,6 +56,8 @@ struct GemmArgs {
   int64_t c_plane;    // STORE / SWIGLU / GLU: C written as 3 bf16 planes instead of fp32
   int64_t c2_plane;   // C2 shadow written as 3 bf16 planes
   int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
+  int res16;          // bf16 / fp8 modes: the residual stream is fp16 -- RESID reads R and writes C as fp16, STORE
+                      // writes C as fp16 (the shadow C2 stays bf16)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -98,6 +100,7 @@ struct MxArgs {
   uint8_t* Q8;            // RESID with C2: also the MXFP8 form of the bf16 shadow, e4m3 [M][ldc] ...
   uint8_t* Q8s;           // ... E8M0 [M][ldc / 32] ...
   float* ss8;             // ... and the rows' sum-of-squares slab [M][kSsSlots]
+  int res16;              // RESID: R and C fp16 (the bf16 / fp8 modes' residual stream)
   int M, N, K;
   int dbg;                // microbenchmarks only (gemm_mx.hip DBG bits); 0 in the session
 };
@@ -168,11 +171,13 @@ hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, 
 // (3 split planes `plane` elements apart when plane > 0).
 // q8 / s8 / ss8 (fp8 mode, optional): also the MXFP8 form of the bf16 shadow row and its sum-of-squares slab,
 // exactly what launch_quant_mx would make from the shadow
-hipError_t launch_rmsnorm(float* x, const float* w, int rows, uint16_t* shadow, int64_t plane, hipStream_t st,
+// r16: x is the bf16 / fp8 modes' fp16 residual stream (read and written as fp16)
+hipError_t launch_rmsnorm(void* x, const float* w, int rows, uint16_t* shadow, int64_t plane, bool r16, hipStream_t st,
                           uint8_t* q8 = nullptr, uint8_t* s8 = nullptr, float* ss8 = nullptr);
 
 // Layers 14/15: xn = RMSNorm(r); kv = [cache(S rows) ; xn]; next cache (left-padded to 30) -> state.
-hipError_t launch_kv_assemble(const float* r, const float* norm_w, StateRef s, int layer_slot, int T, int S,
+// r is the residual stream: fp16 in the bf16 / fp8 modes (obf), fp32 in fp32 mode
+hipError_t launch_kv_assemble(const void* r, const float* norm_w, StateRef s, int layer_slot, int T, int S,
                               void* xn, void* kv, bool obf, int B, hipStream_t st);
 
 struct AttnArgs {
@@ -197,16 +202,18 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
                          int T, int B, hipStream_t st);
 
-// a11: reduction state + grouped conv (384->1536, k3, s2) -> y [B*5][1536]
-hipError_t launch_reduce_conv(const float* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
+// a11: reduction state + grouped conv (384->1536, k3, s2) -> y [B*5][1536]; x fp16 (residual stream) when obf
+hipError_t launch_reduce_conv(const void* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
                               int T, hipStream_t st);
 
-// a12: x10[b*10+t] += x5[b*5+t/2]
-hipError_t launch_upsample_add(float* x10, const float* x5, int B, int T, uint16_t* shadow, int64_t plane, hipStream_t st);
+// a12: x10[b*10+t] += x5[b*5+t/2]; both fp16 (residual stream) when r16
+hipError_t launch_upsample_add(void* x10, const void* x5, int B, int T, uint16_t* shadow, int64_t plane, bool r16,
+                               hipStream_t st);
 
 // a14: logits = x . Wd^T + bd, log_softmax over 35 classes -> logprobs [B*10][35]
 // a14 + decode flags: logprobs [rows][35]; optional frame_info[row] = greedy token | speech flag << 8
-hipError_t launch_head(const float* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows,
+// x: the residual stream, fp16 when r16
+hipError_t launch_head(const void* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows, bool r16,
                        hipStream_t st);
 
 }  // namespace tone

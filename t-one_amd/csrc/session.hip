@@ -416,6 +416,8 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   a.a_bf16 = bf && a_bf16;
   a.c_bf16 = bf && c_bf16;
   a.C2 = bf ? c2 : nullptr;
+  // bf16 / fp8 modes: the residual stream rA / rB is fp16 (the RESID projections, and the STOREs that start it)
+  a.res16 = bf && (epi == EPI_RESID || C == s->rA || C == s->rB);
   if (mx_out) {   // fp8 mode, RESID: also the MXFP8 form of the shadow and its sum-of-squares slab (the next MX GEMM's A)
     a.C8 = s->a8;
     a.C8s = s->a8s;
@@ -453,6 +455,7 @@ int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8,
   a.C8 = C8;
   a.C8s = C8s;
   a.ldc8s = N / 64;
+  a.res16 = epi == EPI_RESID;   // fp8 mode: the residual stream is fp16
   if (mx_out) {   // RESID: also the MXFP8 form of the shadow and its sum-of-squares slab (the next MX GEMM's A)
     a.Q8 = s->a8;
     a.Q8s = s->a8s;
@@ -483,8 +486,9 @@ const void* act_at(const float* base, int64_t i, bool bf) {
 }
 
 // The whole streaming step (Tone.forward_for_export, model.py:162-205).
-// bf16 mode: every GEMM operand is bf16 in memory -- the residual keeps an fp32 master copy plus a
-// bf16 shadow written by each of its producers; the other operands are produced in bf16 directly.
+// bf16 mode: every GEMM operand is bf16 in memory -- the residual stream is kept in fp16 (as the reference's exported
+// graph keeps it) plus a bf16 shadow written by each of its producers; the other operands are produced in bf16 directly.
+// fp32 mode: the residual stream and every activation are fp32.
 int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* logp, int B, hipStream_t st) {
   const int D = kD;
   const bool bf = bfmode(s), f8 = s->precision == TONE_PRECISION_FP8;
@@ -506,7 +510,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   // profiles/r02_fp8_normq_ab.txt)
   const bool f8n = f8 && knobs().fp8_normq;
   bool q8_fresh = f8n;
-  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, st, f8n ? s->a8 : nullptr, s->a8s, s->ss8));
+  LAUNCH("norm", launch_rmsnorm(s->rA, s->out_norm, B * geo.T, shA, 0, bf, st, f8n ? s->a8 : nullptr, s->a8s, s->ss8));
   if (s->debug_stop == 1) {
     // the fused-vs-separate check reads the first FFN1's MXFP8 operand here: make it the separate way too
     if (f8 && !f8n) LAUNCH("quant_mx", launch_quant_mx(shA, D, B * geo.T, D, s->a8, s->a8s, s->ss8, st));
@@ -619,7 +623,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     CALL(ffn(1));
     // the next layer's FFN1 reads this norm's output unless the reduction / upsampling comes in between
     q8_fresh = f8n && l != 6 && l < 14;
-    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->ss8));
+    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, bf, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->ss8));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
       LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, geo.T, st));
       CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * geo.Tr, D, 4 * D,
@@ -629,14 +633,14 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       T = geo.Tr;
     }
     if (l == 14) {  // TemporalUpsampling (conformer.py:224-225)
-      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, geo.T, shA, 0, st));
+      LAUNCH("upsample", launch_upsample_add(s->rA, s->rB, B, geo.T, shA, 0, bf, st));
       x = s->rA;
       xs = shA;
       T = geo.T;
     }
     if (s->debug_stop == 2 + l) return TONE_OK;
   }
-  LAUNCH("head", launch_head(s->rA, s->whead, s->bhead, logp, s->frame_info, B * geo.T, st));
+  LAUNCH("head", launch_head(s->rA, s->whead, s->bhead, logp, s->frame_info, B * geo.T, bf, st));
   return TONE_OK;
 }
 
@@ -1107,8 +1111,25 @@ int tone_session_debug_read(tone_session* s, const char* buffer, void* host_dst,
   if (n == "feats") { p = s->feats; cap = MB * kMelTMax * kMels * 4; }
   else if (n == "x2") { p = s->x2; cap = MB * kSub2InMax * kSub1F * kSub1C * 4; }
   else if (n == "flat") { p = s->flat; cap = MB * kTMax * kSubOut * 4; }
-  else if (n == "rA") { p = s->rA; cap = MB * kTMax * kD * 4; }
-  else if (n == "rB") { p = s->rB; cap = MB * kTrMax * kD * 4; }
+  else if (n == "rA" || n == "rB") {
+    // the residual stream: fp16 in the bf16 / fp8 modes, returned as fp32 like the fp32 mode's
+    const size_t cap_el = MB * (n == "rA" ? kTMax : kTrMax) * kD;
+    if (bytes % 4 || (size_t)bytes / 4 > cap_el) return fail(TONE_E_INVALID, "debug_read larger than the buffer");
+    const float* src = n == "rA" ? s->rA : s->rB;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (!bfmode(s)) {
+      HIP_TRY(hipMemcpy(host_dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
+      return TONE_OK;
+    }
+    std::vector<__half> h((size_t)bytes / 4);
+    HIP_TRY(hipMemcpy(h.data(), src, h.size() * 2, hipMemcpyDeviceToHost));
+    float* d = static_cast<float*>(host_dst);
+    for (size_t i = 0; i < h.size(); ++i) d[i] = __half2float(h[i]);
+    return TONE_OK;
+  }
+  // bf16 / fp8 modes: the bf16 shadow of the residual stream rA (the bits, [M][384])
+  else if (n == "xbA" && s->xbA) { p = s->xbA; cap = MB * kTMax * kD * 2; }
   // fp8 mode: the MXFP8 operand of the next MX GEMM (e4m3 [M][384], E8M0 [M][12], fp32 row factors [M])
   else if (n == "a8" && s->a8) { p = s->a8; cap = MB * kTMax * kD; }
   else if (n == "a8s" && s->a8s) { p = s->a8s; cap = MB * kTMax * (kD / 32); }

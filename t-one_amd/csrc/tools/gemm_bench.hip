@@ -203,7 +203,8 @@ int main(int argc, char** argv) {
   const int M = atoi(argv[1]), K = atoi(argv[2]), N = atoi(argv[3]), epi = atoi(argv[4]);
   const int nsplit = argc > 6 ? atoi(argv[6]) : 1, iters = argc > 7 ? atoi(argv[7]) : 20;
   const int nout = epi >= 2 ? N / 2 : N;
-  const int cbf = epi >= 2 ? 1 : 0;   // as in the session: qkv/attn fp32, SWIGLU/GLU bf16
+  int cbf = epi >= 2 ? 1 : 0;   // as in the session: qkv/attn fp32, SWIGLU/GLU bf16
+  if (getenv("CBF")) cbf = atoi(getenv("CBF"));   // STORE with a bf16 C (output-byte sensitivity of a shape)
   std::vector<uint16_t> hA((size_t)M * K), hW((size_t)N * K);
   std::vector<float> hb(N), hR((size_t)M * N);
   uint64_t x = 12345;
