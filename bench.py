@@ -65,31 +65,36 @@ def family_flops_per_stream(T: int = C.CHUNK_FRAMES) -> dict:
 def family_bytes_per_stream(T: int = C.CHUNK_FRAMES, precision: str = "fp32") -> dict:
     """Algorithmic HBM bytes per stream-chunk of each GEMM family as the session runs it: A read + W read
     (amortised over the batch: added by the caller) + C write, + the residual read/write and the bf16
-    shadow for RESID outputs.  Element sizes follow the precision: fp32 mode reads fp32 activations; bf16
-    mode bf16 activation shadows, bf16 FFN hidden and q/k/v; fp8 mode e4m3 (+1/32 scale) for the FFN and
-    q/k/v operands."""
+    shadow for RESID outputs.  Element sizes follow the precision: fp32 mode reads fp32 activations and an fp32
+    residual stream; bf16 mode bf16 activation shadows, bf16 FFN hidden and q/k/v, and the residual stream in fp16
+    (read + written: 4 B per element, plus the 2 B shadow); fp8 mode as bf16 with e4m3 (+1/32 scale) for the FFN
+    and q/k/v operands, and the RESID epilogues that feed an MX GEMM (FFN1 down of layers 0-13, pw2) also write the
+    shadow's MXFP8 form and its sum-of-squares slab (12 floats per row)."""
     d, ff = C.D_MODEL, C.D_FF
     tr = (T + 1 - 3) // 2 + 1
     lp = precision in ("bf16", "fp8")
+    f8 = precision == "fp8"
     ea = 2 if lp else 4                                   # activation operand
-    e8 = 1 + 1 / 32 if precision == "fp8" else ea         # MX operand (FFN, q/k/v in fp8 mode)
-    eh = 1 + 1 / 32 if precision == "fp8" else ea         # FFN hidden h
-    sh = 2 if lp else 0                                   # bf16 shadow of an fp32 residual output
+    e8 = 1 + 1 / 32 if f8 else ea                         # MX operand (FFN, q/k/v in fp8 mode)
+    eh = 1 + 1 / 32 if f8 else ea                         # FFN hidden h
+    sh = 2 if lp else 0                                   # bf16 shadow of a residual output
+    er = 2 if lp else 4                                   # residual stream element (fp16 / fp32)
+    q8 = (1 + 1 / 32 + 4 * 12 / d) if f8 else 0.0         # MXFP8 shadow + sum-of-squares slab, per element
     f = {k: 0.0 for k in GEMM_FAMILIES}
     for l in range(C.N_LAYERS):
         t = tr if C.REDUCTION_POS < l <= C.UPSAMPLE_POS else T
         s = C.mhsa_cache_rows(l)
         f["gemm_ffn_up"] += 2 * t * (d * e8 + ff * eh)
-        f["gemm_ffn_down"] += 2 * t * (ff * eh + d * (8 + sh))
+        f["gemm_ffn_down"] += 2 * t * (ff * eh + d * (2 * er + sh)) + (t * d * q8 if l < C.MHSA_STATELESS else 0)
         if l < C.MHSA_STATELESS:
             f["gemm_qkv"] += t * d * (e8 + (3 if C.RECOMPUTE_SCORES[l] else 1) * ea)
         else:
             f["gemm_qkv"] += t * d * (e8 + ea) + (s + t) * d * (e8 + 2 * ea)
-        f["gemm_attn_out"] += t * d * (ea + 8 + sh)
+        f["gemm_attn_out"] += t * d * (ea + 2 * er + sh)
         f["gemm_pw1"] += t * d * (ea + 4)
-        f["gemm_pw2"] += t * d * (ea + 8 + sh)
-    f["gemm_sub_out"] = T * (C.SUB_OUT_IN * ea + d * 4)
-    f["gemm_reduce"] = tr * (4 * d * ea + d * (4 + sh))
+        f["gemm_pw2"] += t * d * (ea + 2 * er + sh + q8)
+    f["gemm_sub_out"] = T * (C.SUB_OUT_IN * ea + d * er)
+    f["gemm_reduce"] = tr * (4 * d * ea + d * (er + sh))
     return f
 
 

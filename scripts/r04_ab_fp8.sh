@@ -1,0 +1,20 @@
+# fp8 B = 4096 A/B of two library builds (base = TONEHIP_LIB=t-one_amd/libtonehip_base.so), then the fp8 GPU tests
+set -u
+export TMPDIR=/tmp
+out=gpurun_out/r04_ab_fp8.jsonl
+mkdir -p gpurun_out
+: > $out
+for rep in 1 2 3; do
+  for lib in base cur; do
+    if [ $lib = base ]; then export TONEHIP_LIB=t-one_amd/libtonehip_base.so; else unset TONEHIP_LIB; fi
+    timeout -k 10 240 python bench.py --precision fp8 --batch 4096 --steps 100 --warmup 3 --alt 0 --config4 0 --config5 0 \
+      --cpu-baseline-s 0 > gpurun_out/ab_leg.json 2> gpurun_out/ab_leg.err || { tail -5 gpurun_out/ab_leg.err; exit 1; }
+    python3 -c "
+import json; d=json.load(open('gpurun_out/ab_leg.json'))
+print(json.dumps({'lib': '$lib', 'rep': $rep, 'ms_per_step': d['ms_per_step']}))" >> $out
+    tail -1 $out
+  done
+done
+unset TONEHIP_LIB
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "fp8" --timeout 300 --timeout-method thread > gpurun_out/r04_fp8_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r04_fp8_tests.log; exit $rc

@@ -8,14 +8,14 @@ import csv, glob, json, re, sys
 
 root, prec, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
 UP = {  # SWIGLU instantiations: EPI_SWIGLU = 2
-    "fp32": r"gemm_x3_kernel<tone::XT<[^>]*>, 2,",
-    "fp32-mfma": r"gemm_kernel<tone::Tile<[^>]*>, 2,",
-    "bf16": r"(gemm_t_kernel<tone::TT<[^>]*>, 2,|gemm_x[sw]\d?_kernel<2, )",
+    "fp32": r"gemm_x3_kernel<tone::(?:\(anonymous namespace\)::)?XT<[^>]*>, 2,",
+    "fp32-mfma": r"gemm_kernel<tone::(?:\(anonymous namespace\)::)?Tile<[^>]*>, 2,",
+    "bf16": r"(gemm_t_kernel<tone::(?:\(anonymous namespace\)::)?TT<[^>]*>, 2,|gemm_x[sw]\d?_kernel<2, )",
     "fp8": r"(gemm_xs8_kernel<2, |gemm_mx_kernel<\d+, 2, )",
 }[prec]
 # EPI_RESID = 1, in any GEMM kernel family
-RESID = (r"(gemm_x3_kernel<tone::XT<[^>]*>, 1,|gemm_glds_kernel<tone::Tile<[^>]*>, 1,|gemm_kernel<tone::Tile<[^>]*>, 1,"
-         r"|gemm_t_kernel<tone::TT<[^>]*>, 1,|gemm_f32t_kernel<[^>]*>, 1,|gemm_mx_kernel<\d+, 1,)")
+RESID = (r"(gemm_x3_kernel<tone::(?:\(anonymous namespace\)::)?XT<[^>]*>, 1,|gemm_glds_kernel<tone::(?:\(anonymous namespace\)::)?Tile<[^>]*>, 1,|gemm_kernel<tone::(?:\(anonymous namespace\)::)?Tile<[^>]*>, 1,"
+         r"|gemm_t_kernel<tone::(?:\(anonymous namespace\)::)?TT<[^>]*>, 1,|gemm_f32t_kernel<[^>]*>, 1,|gemm_mx_kernel<\d+, 1,)")
 
 
 def per_launch(sub, pat):

@@ -51,15 +51,19 @@ def test_algo_bytes_per_launch_by_precision():
 
 def test_algo_bytes_resid_family():
     """The EPI_RESID family (FFN down, attn-out, pw2 as one kernel family, 64 launches per step): A read at
-    the operand size, the fp32 residual read and written, the bf16 shadow (bf16 / fp8 modes), W once."""
+    the operand size, the residual stream read and written (fp32 in fp32 mode, fp16 in the bf16 / fp8 modes), the
+    bf16 shadow (bf16 / fp8 modes), in fp8 mode the MXFP8 shadow + sum-of-squares slab written by FFN1 down of layers
+    0-13 and by pw2, W once."""
     d, ff, B = 384, 1536, 2048
-    tot = 0.0
-    for prec, ea, eh, sh in (("bf16", 2, 2, 2), ("fp8", 2, 1 + 1 / 32, 2), ("fp32", 4, 4, 0)):
+    for prec, ea, eh, er, sh in (("bf16", 2, 2, 2, 2), ("fp8", 2, 1 + 1 / 32, 2, 2), ("fp32", 4, 4, 4, 0)):
+        q8 = (1 + 1 / 32 + 48 / d) if prec == "fp8" else 0.0
         tot = 0.0
         for l in range(16):
             rows = B * (5 if 6 < l <= 14 else 10)
-            tot += 2 * rows * (ff * eh + d * (8 + sh))         # two FFN downs
-            tot += 2 * rows * (d * ea + d * (8 + sh))          # attn-out + pw2
+            tot += 2 * rows * (ff * eh + d * (2 * er + sh))    # two FFN downs
+            tot += rows * d * q8 if l < 14 else 0.0            # FFN1 down feeds q|k|v (fp8)
+            tot += 2 * rows * (d * ea + d * (2 * er + sh))     # attn-out + pw2
+            tot += rows * d * q8                               # pw2 feeds FFN2 (fp8)
         ew, e8 = (4, 4) if prec == "fp32" else (2, eh)
         tot += 16 * (2 * ff * d * e8 + 2 * d * d * ew)
         got = bench.algo_bytes("resid", prec, B)
