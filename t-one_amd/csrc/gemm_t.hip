@@ -740,9 +740,9 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
 template <class TL, int EPI>
 hipError_t launch_x3(const GemmArgs& a0, hipStream_t st) {
   GemmArgs a = a0;
-  // static priority for waves NW/2.. (default; TONE_X3_PRIO=0 turns it off): fp32 B = 256 step 3.616 -> 3.583 ms,
-  // FFN down 897 -> 871 us (profiles/r02_ab_x3_prio.jsonl)
-  if (knobs().x3_prio) a.dbg |= 64;
+  // static priority for waves NW/2..: fp32 B = 256 step 3.616 -> 3.583 ms, FFN down 897 -> 871 us
+  // (profiles/r02_ab_x3_prio.jsonl)
+  a.dbg |= 64;
   const dim3 tiles((a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX), a.k_split ? a.K / a.k_split : 1);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
   if (a.a_plane) {

@@ -12,7 +12,6 @@ namespace tone {
 // Experiment switches, read from the environment ONCE per process (the first call; A/B runs compare separate
 // processes).  Defaults are the measured best; none of them changes the arithmetic.
 struct Knobs {
-  int x3_prio;         // TONE_X3_PRIO=0: no static priority in gemm_x3 (default on)
   int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand
 };
 const Knobs& knobs();

@@ -31,7 +31,6 @@ const Knobs& knobs() {
       return e && *e ? std::atoi(e) : dflt;
     };
     Knobs r;
-    r.x3_prio = env("TONE_X3_PRIO", 1) != 0;
     r.fp8_normq = env("TONE_FP8_NORMQ", 1) != 0;
     return r;
   }();

@@ -86,7 +86,8 @@ __global__ void err_kernel(const void* C, int cbf, const float* ref, int64_t n, 
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float e = 0.f;
   for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float c = cbf ? bf(static_cast<const uint16_t*>(C)[i]) : static_cast<const float*>(C)[i];
+    const float c = cbf == 2 ? __half2float(static_cast<const __half*>(C)[i])
+                    : cbf ? bf(static_cast<const uint16_t*>(C)[i]) : static_cast<const float*>(C)[i];
     const float r = ref[i];
     e = fmaxf(e, fabsf(c - r) / (1.f + fabsf(r)));
   }
@@ -274,6 +275,17 @@ int main(int argc, char** argv) {
   a.M = M; a.N = N; a.K = K; a.ws = ws; a.ws_ss = ws_ss; a.ws_cap = ws_cap; a.a_bf16 = 1; a.c_bf16 = cbf;
   a.C2 = (epi == 1 || (epi == 0 && !cbf)) ? C2 : nullptr;   // the session's shadowed outputs
   if (getenv("NOC2")) a.C2 = nullptr;                         // fp32 mode: no bf16 shadow
+  // RES16=1: the bf16 / fp8 modes' fp16 residual stream (R and C fp16; the reference keeps its fp32 R)
+  const bool res16 = getenv("RES16") && atoi(getenv("RES16"));
+  __half* R16 = nullptr;
+  if (res16) {
+    std::vector<__half> h(hR.size());
+    for (size_t i = 0; i < h.size(); ++i) h[i] = __float2half(hR[i]);
+    CK(hipMalloc(&R16, h.size() * 2));
+    CK(hipMemcpy(R16, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    a.R = reinterpret_cast<const float*>(R16);
+    a.res16 = 1;
+  }
   a.rowscale = rowscale;
   a.inv_sqrt_k = 1.0f / sqrtf((float)K);
   hipEvent_t e0, e1;
@@ -304,6 +316,7 @@ int main(int argc, char** argv) {
     a.W = f32 ? (const void*)Wf : (const void*)W;
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
+    a.res16 = res16 && !f32;
     auto launch = [&]() {
       return vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
@@ -320,7 +333,7 @@ int main(int argc, char** argv) {
     if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", v, hipGetErrorString(rc)); continue; }
     CK(hipDeviceSynchronize());
     CK(hipMemset(err, 0, 4));
-    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, a.c_bf16, ref, (int64_t)M * nout, err);
+    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, a.res16 && epi <= 1 ? 2 : a.c_bf16, ref, (int64_t)M * nout, err);
     float herr, herr2 = 0.f;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
     if (a.C2) {   // the bf16 shadow must hold the same values (bf16-rounded)
