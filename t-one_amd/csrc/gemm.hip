@@ -901,7 +901,10 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st, bool* c8
   // profiles/r03_xs_route_sweep.jsonl; round 4's gemm_xw 1.8 % / 3 % below gemm_xs in the bf16 B = 4096 step,
   // profiles/r04_xw_step_ab.json)
   const int xblocks = (a.M + 255) / 256;
-  if (a.K == 384 && ((epi == EPI_SWIGLU && xblocks >= 40) || (epi == EPI_GLU && xblocks >= 60))) {
+  // ... and the K = 384 bf16-output STOREs of N >= 768 (q|k|v of layers 0 / 7, k|v of layers 14 / 15) from 80 blocks:
+  // M = 40960, N = 1152: 56 vs 74 us; N = 384 stays on the LDS-DMA tiles (29 vs 27 us; profiles/r04_xw_store.jsonl)
+  if (a.K == 384 && ((epi == EPI_SWIGLU && xblocks >= 40) || (epi == EPI_GLU && xblocks >= 60) ||
+                     (epi == EPI_STORE && a.c_bf16 && !a.C2 && a.N >= 768 && xblocks >= 80))) {
     const hipError_t e = gemm_xw(a, epi, 0, st);
     if (e != hipErrorInvalidValue) return e;   // shape outside gemm_xw's contract: the routes below
   }

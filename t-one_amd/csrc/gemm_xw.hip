@@ -39,7 +39,10 @@ constexpr int kXwRowB = kXwK * 2;            // bytes per W row
 constexpr int kXwTile = kXwBN * kXwRowB;     // 48 KiB
 constexpr int kXwR = 3;                      // ring depth
 constexpr int kXwP = kXwTile / 1024 / kXwWaves;   // 1 KiB DMA pieces per wave per tile (6)
-constexpr int kXwS = 2;                      // stores per lane per step (the previous step's epilogue)
+// stores per lane per step (the previous step's epilogue): SwiGLU / GLU 2 (16 hidden columns), STORE 4 (the g and u
+// halves of the tile are both outputs)
+template <int EPI>
+constexpr int xw_stores() { return EPI == EPI_STORE ? 4 : 2; }
 
 typedef __bf16 xw_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float xw_f32x16 __attribute__((ext_vector_type(16)));
@@ -63,7 +66,8 @@ struct XwPos {
 // (profiles/r04_xw_ablate.jsonl): the ping-pong is 7-8 % slower than the interleaved schedule.
 template <int EPI, bool RS, int DBG = 0>
 __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, int nc) {
-  static_assert(EPI == EPI_SWIGLU || EPI == EPI_GLU, "SWIGLU / GLU");
+  static_assert(EPI == EPI_SWIGLU || EPI == EPI_GLU || EPI == EPI_STORE, "SWIGLU / GLU / STORE");
+  constexpr int kXwS = xw_stores<EPI>();
   __shared__ __attribute__((aligned(16))) uint8_t lds[kXwR * kXwTile + 4 * kBiasMax];
   float* sbias = reinterpret_cast<float*>(lds + kXwR * kXwTile);
 
@@ -146,25 +150,42 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   };
 
   xw_f32x16 acc[2][2];       // [buffer][g, u]
-  uint32_t po[8];            // packed bf16 pairs of the epilogue in flight
+  uint32_t po[8], pu[8];     // packed bf16 pairs of the epilogue in flight (pu: STORE's second half)
   // epilogue part k (registers 2k, 2k + 1) of the step held in buffer b: W tile t, output row mrow, row factor inv
   auto epi_part = [&](int b, int t, int64_t mrow, float inv, int k) __attribute__((always_inline)) {
     const int u = 16 * (k >> 2) + 8 * lh + 2 * (k & 3);              // hidden column of register 2k within the tile
     const xw_f32x2 bg = *reinterpret_cast<const xw_f32x2*>(sbias + kXwBN * t + u);
     const xw_f32x2 bu = *reinterpret_cast<const xw_f32x2*>(sbias + kXwBN * t + 32 + u);
-    float y[2];
+    if constexpr (EPI == EPI_STORE) {
+      // output columns 64 t + u, + 1 (rows 0-31 of the tile) and 64 t + 32 + u, + 1 (rows 32-63): bias, row factor
+      float y[2], z[2];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {   // scalar fp32 (packed f32 VALU beside MFMAs costs more than two plain ops)
-      const float g = fmaf(acc[b][0][2 * k + e], inv, bg[e]);
-      const float v = fmaf(acc[b][1][2 * k + e], inv, bu[e]);
-      const float z = (EPI == EPI_SWIGLU) ? g : v;               // the sigmoid's argument
-      const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
-      y[e] = (EPI == EPI_SWIGLU) ? g * sg * v : g * sg;
-    }
-    po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{y[0], y[1]}, xw_bf16x2));
-    if ((k & 3) == 3) {   // registers 0-7 / 8-15 done: 8 consecutive hidden columns, one 16-byte store
-      const xw_u32x4 w = {po[k - 3], po[k - 2], po[k - 1], po[k]};
-      *reinterpret_cast<xw_u32x4*>(Cout + mrow * p.ldc + 32 * t + 16 * (k >> 2) + 8 * lh) = w;
+      for (int e = 0; e < 2; ++e) {
+        y[e] = fmaf(acc[b][0][2 * k + e], inv, bg[e]);
+        z[e] = fmaf(acc[b][1][2 * k + e], inv, bu[e]);
+      }
+      po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{y[0], y[1]}, xw_bf16x2));
+      pu[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{z[0], z[1]}, xw_bf16x2));
+      if ((k & 3) == 3) {   // 8 consecutive columns of each half: two 16-byte stores
+        uint16_t* dst = Cout + mrow * p.ldc + kXwBN * t + 16 * (k >> 2) + 8 * lh;
+        *reinterpret_cast<xw_u32x4*>(dst) = xw_u32x4{po[k - 3], po[k - 2], po[k - 1], po[k]};
+        *reinterpret_cast<xw_u32x4*>(dst + 32) = xw_u32x4{pu[k - 3], pu[k - 2], pu[k - 1], pu[k]};
+      }
+    } else {
+      float y[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {   // scalar fp32 (packed f32 VALU beside MFMAs costs more than two plain ops)
+        const float g = fmaf(acc[b][0][2 * k + e], inv, bg[e]);
+        const float v = fmaf(acc[b][1][2 * k + e], inv, bu[e]);
+        const float z = (EPI == EPI_SWIGLU) ? g : v;               // the sigmoid's argument
+        const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
+        y[e] = (EPI == EPI_SWIGLU) ? g * sg * v : g * sg;
+      }
+      po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{y[0], y[1]}, xw_bf16x2));
+      if ((k & 3) == 3) {   // registers 0-7 / 8-15 done: 8 consecutive hidden columns, one 16-byte store
+        const xw_u32x4 w = {po[k - 3], po[k - 2], po[k - 1], po[k]};
+        *reinterpret_cast<xw_u32x4*>(Cout + mrow * p.ldc + 32 * t + 16 * (k >> 2) + 8 * lh) = w;
+      }
     }
   };
 
@@ -197,10 +218,11 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
       __builtin_amdgcn_s_waitcnt(0x0F70);                         // vmcnt(0) expcnt(7) lgkmcnt(15)
     } else {
       // ring slot s landed: step s's DMA went out one piece at a time during step s - 2 (every four K-steps, or
-      // between the epilogue parts of the ping-pong's VALU phase), its last piece before that step's second store;
-      // younger ops: that store, step s - 1's pieces (tile s + 1) and its two stores
-      const int younger = (s >= 3) + (s + 1 < total ? kXwP : 0) + kXwS * (s >= 2);
-      if (younger == 1 + kXwP + kXwS) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      // between the epilogue parts of the ping-pong's VALU phase), its last piece before that step's last epilogue
+      // part; younger ops: that part's stores, step s - 1's pieces (tile s + 1) and its stores
+      constexpr int kLate = kXwS / 2;
+      const int younger = kLate * (s >= 3) + (s + 1 < total ? kXwP : 0) + kXwS * (s >= 2);
+      if (younger == kLate + kXwP + kXwS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLate + kXwP + kXwS) : "memory");
       else vmcnt_dyn(younger);
     }
     barrier_lds();                                                // ... for every wave; slot (s + 2) % 3 free
@@ -340,7 +362,7 @@ hipError_t launch_xw(const GemmArgs& a, int nc, hipStream_t st) {
 
 }  // namespace
 
-// nc = W tiles per work item, an even divisor of N / 64 (0: xw_run_length); SWIGLU / GLU with bf16 output only
+// nc = W tiles per work item, an even divisor of N / 64 (0: xw_run_length); SWIGLU / GLU / STORE with bf16 output only
 hipError_t gemm_xw(const GemmArgs& a, int epi, int nc, hipStream_t st) {
   if (!a.a_bf16 || !a.c_bf16 || a.K != kXwK || a.N % kXwBN || a.N > kBiasMax || a.M <= 0 || a.rpg || a.lda % 8 ||
       a.ldc % 8 || a.k_split || a.C2)
@@ -351,6 +373,7 @@ hipError_t gemm_xw(const GemmArgs& a, int epi, int nc, hipStream_t st) {
   switch (epi) {
     case EPI_SWIGLU: return launch_xw<EPI_SWIGLU>(a, nc, st);
     case EPI_GLU: return launch_xw<EPI_GLU>(a, nc, st);
+    case EPI_STORE: return launch_xw<EPI_STORE>(a, nc, st);
     default: return hipErrorInvalidValue;
   }
 }
