@@ -444,25 +444,39 @@ hipError_t launch_reduce_conv(const void* x, StateRef s, const float* w, const f
 template <bool R16>
 __global__ void __launch_bounds__(256) upsample_add_kernel(void* __restrict__ x10, const void* __restrict__ x5, int B,
                                                            int T, int Tr, uint16_t* __restrict__ shadow, int64_t plane) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // four consecutive channels per thread (8-byte fp16 / 16-byte fp32 residual vectors, 8-byte bf16 shadow)
+  const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (idx >= (int64_t)B * T * kD) return;
   const int64_t row = idx / kD;
   const int c = idx % kD;
   const int64_t b = row / T, t = row % T;
-  const float v = (t < 2 * Tr ? load_res<R16>(x5, (b * Tr + t / 2) * kD + c) : 0.0f) + load_res<R16>(x10, idx);
-  store_res<R16>(x10, idx, v);
-  if (shadow) store_shadow(shadow, plane, idx, v);
+  f32x4_t v = load_res4(x10, idx, R16);
+  if (t < 2 * Tr) v += load_res4(x5, (b * Tr + t / 2) * kD + c, R16);
+  store_res4(x10, idx, v, R16);
+  if (shadow) {
+    if (!plane) {
+      const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+      *reinterpret_cast<uint2*>(shadow + idx) =
+          make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16),
+                     (uint32_t)__builtin_bit_cast(uint16_t, h2) | ((uint32_t)__builtin_bit_cast(uint16_t, h3) << 16));
+    } else {
+      store_shadow(shadow, plane, idx, v.x);
+      store_shadow(shadow, plane, idx + 1, v.y);
+      store_shadow(shadow, plane, idx + 2, v.z);
+      store_shadow(shadow, plane, idx + 3, v.w);
+    }
+  }
 }
 
 hipError_t launch_upsample_add(void* x10, const void* x5, int B, int T, uint16_t* shadow, int64_t plane, bool r16,
                                hipStream_t st) {
-  const int64_t n = (int64_t)B * T * kD;
+  const int64_t n4 = (int64_t)B * T * kD / 4;
   const int Tr = (T + 1 - 3) / 2 + 1;
   if (r16)
-    hipLaunchKernelGGL(upsample_add_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
+    hipLaunchKernelGGL(upsample_add_kernel<true>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
                        shadow, plane);
   else
-    hipLaunchKernelGGL(upsample_add_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
+    hipLaunchKernelGGL(upsample_add_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
                        shadow, plane);
   return hipGetLastError();
 }
