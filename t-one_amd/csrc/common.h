@@ -5,7 +5,20 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace tone {
+
+// f(std::integral_constant<int, I>) for I = 0 .. N-1, each call its own instantiation: loops whose index must be a
+// compile-time constant but whose body is past the unroller's size limit
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // ---- model constants (t-one_amd/config.py; tone/training/model_wrapper.py:27-115) -------------
 constexpr int kChunk = 2400;                  // 300 ms (the defaults below; 400 ms: Geom)

@@ -323,11 +323,15 @@ __global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restr
                                                          uint16_t* __restrict__ flat) {
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
   typedef float f32x4 __attribute__((ext_vector_type(4)));
-  // ONE LDS object: slab | 3 ring slots | scale | shift
-  __shared__ __attribute__((aligned(16))) float lds[kC2Slab + 3 * kC2Ring + 2 * kSub2C];
-  float* ring = lds + kC2Slab;
-  float* sc = ring + 3 * kC2Ring;
+  // ONE LDS object: 3 ring slots | slab | scale | shift.  The ring comes first so that every fragment read of the
+  // unrolled tap loop is a per-lane VGPR base plus a compile-time immediate below 64 KiB: the ring slot and tap
+  // (slot * 16 KiB + u * 4 KiB) for the weights, the tap's input offset toff * 64 B for the slab.
+  __shared__ __attribute__((aligned(16))) float lds[3 * kC2Ring + kC2Slab + 2 * kSub2C];
+  float* ring = lds;
+  float* slab = lds + 3 * kC2Ring;
+  float* sc = slab + kC2Slab;
   float* sh = sc + kSub2C;
+  const char* lb = reinterpret_cast<const char*>(lds);
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint16_t* xb = x2 + (int64_t)b * kC2In * kSub1C;
   if (tid < kSub2C) {
@@ -346,6 +350,7 @@ __global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restr
       __builtin_amdgcn_global_load_lds(src, ring + (sg % 3) * kC2Ring + pc * 256, 16, 0, 0);
 #else
       (void)src;
+      (void)ring;
 #endif
     }
   };
@@ -353,7 +358,7 @@ __global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restr
     const int L = pc * 64 + lane, q = min(L >> 2, kC2In - 1), s = L & 3;
     const uint16_t* src = xb + q * kSub1C + ((s ^ c2_swz(q)) << 3);
 #if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src, lds + pc * 256, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(src, slab + pc * 256, 16, 0, 0);
 #else
     (void)src;
 #endif
@@ -361,58 +366,60 @@ __global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restr
   stage_taps(0);
   stage_taps(1);
 
-  // per position tile: the lane's output position and its input base position
+  // Per-lane byte offsets, computed once.  Slab position q = qb + toff (qb: the lane's output position's first input
+  // position, toff = kt * 44 + kf: the tap) is read at q * 64 B + 16 B * (g ^ swz(q)); swz depends on bit 2 of q only,
+  // i.e. on (qb + (toff & 7)) & 4, so xa[i][c] holds the offset for toff & 7 == c and the tap adds toff * 64 B as an
+  // immediate.  Waves 6-7 own 2 of the 22 position tiles: their third tile repeats position 339 (its MFMAs keep
+  // every SIMD at 6 tiles, which the other SIMDs need anyway, and keep the unrolled loop free of branches).
   const int n = lane & 15, g = lane >> 4;
-  int qb[3];
+  uint32_t xa[3][8], wa[4];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int p = min((wid + 8 * i) * 16 + n, kC2Pos - 1);
-    qb[i] = (kSub2Stride * (p / kSub2F)) * kSub1F + p % kSub2F;
+    const int qb = (kSub2Stride * (p / kSub2F)) * kSub1F + p % kSub2F;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) xa[i][c] = (uint32_t)((3 * kC2Ring + qb * 16 + ((g ^ c2_swz(qb + c)) << 2)) * 4);
   }
-  const int ntile = wid < 6 ? 3 : 2;                      // 22 tiles over 8 waves (wave-uniform)
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int row = 16 * c + n;
+    wa[c] = (uint32_t)((row * 16 + ((g ^ c2_swz(row)) << 2)) * 4);
+  }
   f32x4 acc[3][4];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int sg = 0; sg < kC2Stages; ++sg) {
-    if (sg + 1 < kC2Stages) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  // every stage is its own instantiation (a 31-stage loop is past the unroller's size limit, and a runtime stage
+  // index would turn xa[i][toff & 7] into a scratch-memory lookup).  Reading the next tap's fragments ahead of
+  // this tap's MFMAs by hand measured no faster: the scheduler already interleaves them.
+  static_for<kC2Stages>([&](auto sgc) {
+    constexpr int sg = decltype(sgc)::value;
+    if constexpr (sg + 1 < kC2Stages) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_lds_c2();                                      // stage sg (and the slab) landed; slot (sg+2)%3 free
-    if (sg + 2 < kC2Stages) stage_taps(sg + 2);
-    const float* wst = ring + (sg % 3) * kC2Ring;
-    const int ntap = min(kC2TP, kC2Taps - sg * kC2TP);     // uniform
+    if constexpr (sg + 2 < kC2Stages) stage_taps(sg + 2);
 #pragma unroll
     for (int u = 0; u < kC2TP; ++u) {
-      if (u >= ntap) break;
       const int j = sg * kC2TP + u;
-      const float* wr = wst + u * 1024;
-      const int kt = j / kSub2Kf, kf = j % kSub2Kf, toff = kt * kSub1F + kf;
+      if (j >= kC2Taps) break;
+      const int toff = (j / kSub2Kf) * kSub1F + j % kSub2Kf;
+      const int woff = ((sg % 3) * kC2Ring + u * 1024) * 4;
       bf16x8 wf[4], xf[3];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int row = 16 * c + n;
-        wf[c] = *reinterpret_cast<const bf16x8*>(wr + row * 16 + ((g ^ c2_swz(row)) << 2));
-      }
+      for (int c = 0; c < 4; ++c) wf[c] = *reinterpret_cast<const bf16x8*>(lb + wa[c] + woff);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int q = qb[i] + toff;
-        xf[i] = *reinterpret_cast<const bf16x8*>(lds + q * 16 + ((g ^ c2_swz(q)) << 2));
-      }
+      for (int i = 0; i < 3; ++i) xf[i] = *reinterpret_cast<const bf16x8*>(lb + xa[i][toff & 7] + toff * 64);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        if (i < ntile) {
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], xf[i], acc[i][c], 0, 0, 0);
-        }
-      }
+        for (int c = 0; c < 4; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], xf[i], acc[i][c], 0, 0, 0);
     }
-  }
+  });
   // epilogue: D[channel][position]; lane: position 16 tile + n, channels 16 c + 4 g + r
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    if (i >= ntile) break;
     const int p = (wid + 8 * i) * 16 + n;
     if (p >= kC2Pos) continue;
     uint16_t* dst = flat + ((int64_t)b * kC2Pos + p) * kSub2C;
