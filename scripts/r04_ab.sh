@@ -1,12 +1,14 @@
-# A/B of two library builds on the large-batch legs: TONEHIP_LIB=t-one_amd/libtonehip_base.so (A) vs the tree's
-# libtonehip.so (B), alternating, one bench process per leg -> gpurun_out/r04_ab_<tag>.jsonl
+# A/B of two library builds on the large-batch legs (or LEGS="precision batch;..."): TONEHIP_LIB=
+# t-one_amd/libtonehip_base.so (A) vs the tree's libtonehip.so (B), alternating, one bench process per leg
+# -> gpurun_out/r04_ab_<tag>.jsonl
 set -u
 tag=${1:-ab}
 out=gpurun_out/r04_ab_$tag.jsonl
 mkdir -p gpurun_out
 : > $out
 for rep in 1 2; do
-  for leg in "bf16 4096" "fp8 4096" "bf16 2048"; do
+  IFS=';' read -ra legs <<< "${LEGS:-bf16 4096;fp8 4096;bf16 2048}"
+  for leg in "${legs[@]}"; do
     set -- $leg
     for lib in base cur; do
       if [ $lib = base ]; then export TONEHIP_LIB=t-one_amd/libtonehip_base.so; else unset TONEHIP_LIB; fi

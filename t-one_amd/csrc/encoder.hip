@@ -125,116 +125,26 @@ hipError_t launch_kv_assemble(const void* r, const float* norm_w, StateRef s, in
 // ---------------------------------------------------------------------------------------------
 // RotaryMultiHeadAttention.forward (conformer_blocks.py:688-726) + forward_qkv/forward_attention
 // (submodules.py:204-271).  One wave per (stream, head), four heads per 256-thread workgroup;
-// every wave works in its own small LDS slice, so the kernel has no workgroup barrier.  T (query
-// rows) and S (cached rows; TK = S + T keys) are template parameters so every per-lane array stays
-// in registers.
-//   recompute: key row j lives in lane j (its 48 dims in registers): per-head LayerNorm(48,
-//              eps 1e-5) and RoPE on dims [0,32) (rotate_half pairs d, d+16; k at positions
-//              -S..T-1) run in-lane; the T query rows get the same treatment in lanes 0..T-1 and
-//              go to LDS; lane j then computes scores q_i . k_j / sqrt(48) for every i, applies the
-//              layer 14/15 masks, and the softmax over j is a wave reduction per query row.
-//   shared   : probabilities of the last recomputing layer (no mask in layers 1-6 / 8-13, so
-//              softmax(shared scores) = shared probabilities), read from the probs buffer.
-//   ctx = P . V: lane c < 48 owns output column c; its TK values of V are loaded straight into
-//   registers at kernel start (one coalesced row per load), P rows are read from LDS as
-//   broadcast float4s, the T output rows accumulate independently.
-
-template <int T, int S, bool REC, bool OBF>
+// every wave works in its own small LDS slice, so the kernel has no workgroup barrier.
+//   shared layers (this kernel): probabilities of the last recomputing layer (no mask in layers 1-6 / 8-13, so
+//   softmax(shared scores) = shared probabilities), read from the probs buffer; ctx = P . V: lane c < 48 owns output
+//   column c, its T values of V are loaded straight into registers at kernel start (one coalesced row per load), P
+//   rows are read from LDS as broadcast float4s, the T output rows accumulate independently.
+//   recomputing layers: attention_rec_kernel below (LayerNorm + RoPE + scores + softmax + P . V).
+template <int T, bool OBF>
 __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
-  constexpr int TK = S + T, TKP = (TK + 3) & ~3;
-  __shared__ __attribute__((aligned(16))) float sm[4][T * kDk + T * TKP];
+  constexpr int TK = T, TKP = (TK + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) float sm[4][T * TKP];
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int b = blockIdx.x >> 1, h = ((blockIdx.x & 1) << 2) + wid;
-  float* qs = sm[wid];                        // [T][48]
-  float* ps = qs + T * kDk;                   // [T][TKP]
+  float* ps = sm[wid];                        // [T][TKP]
   const int c0 = h * kDk;
   const int cl = min(lane, kDk - 1);
   float vr[TK];                               // V column cl, all keys (issued first: in flight meanwhile)
 #pragma unroll
   for (int j = 0; j < TK; ++j) vr[j] = load_act<OBF>(a.v, ((int64_t)b * TK + j) * a.ldv + c0 + cl);
-  if constexpr (REC) {
-    // LayerNorm + RoPE of one 48-dim row held in registers; pos = RoPE position
-    auto ln_rope = [&](float (&x)[kDk], const float* lw, const float* lb, int pos) {
-      float mu = 0.f;
-#pragma unroll
-      for (int d = 0; d < kDk; ++d) mu += x[d];
-      mu *= (1.0f / kDk);
-      float var = 0.f;
-#pragma unroll
-      for (int d = 0; d < kDk; ++d) {
-        x[d] -= mu;
-        var += x[d] * x[d];
-      }
-      const float rstd = 1.0f / sqrtf(var * (1.0f / kDk) + kLnEps);
-#pragma unroll
-      for (int d = 0; d < kDk; ++d) x[d] = x[d] * rstd * lw[d] + lb[d];
-      const float* cs = a.rope_cos + (pos + kMhsaS) * (kRope / 2);
-      const float* sn = a.rope_sin + (pos + kMhsaS) * (kRope / 2);
-#pragma unroll
-      for (int d = 0; d < kRope / 2; ++d) {            // rotate_half pairs (d, d+16), submodules.py:142-157
-        const float y0 = x[d], y1 = x[d + 16];
-        x[d] = y0 * cs[d] - y1 * sn[d];
-        x[d + 16] = y1 * cs[d] + y0 * sn[d];
-      }
-    };
-    if (lane < T) {   // query rows first (their registers are free again before the key rows load)
-      float qr[kDk];
-#pragma unroll
-      for (int c4 = 0; c4 < kDk / 4; ++c4) {
-        const float4 v = load_act4<OBF>(a.q, ((int64_t)b * T + lane) * a.ldq + c0 + 4 * c4);
-        qr[4 * c4] = v.x; qr[4 * c4 + 1] = v.y; qr[4 * c4 + 2] = v.z; qr[4 * c4 + 3] = v.w;
-      }
-      ln_rope(qr, a.qln_w, a.qln_b, lane);
-#pragma unroll
-      for (int c4 = 0; c4 < kDk / 4; ++c4)
-        *reinterpret_cast<float4*>(qs + lane * kDk + 4 * c4) = make_float4(qr[4 * c4], qr[4 * c4 + 1], qr[4 * c4 + 2], qr[4 * c4 + 3]);
-    }
-    float kr[kDk];
-    const int jr = min(lane, TK - 1);
-#pragma unroll
-    for (int c4 = 0; c4 < kDk / 4; ++c4) {
-      const float4 v = load_act4<OBF>(a.k, ((int64_t)b * TK + jr) * a.ldk + c0 + 4 * c4);
-      kr[4 * c4] = v.x; kr[4 * c4 + 1] = v.y; kr[4 * c4 + 2] = v.z; kr[4 * c4 + 3] = v.w;
-    }
-    ln_rope(kr, a.kln_w, a.kln_b, jr - S);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float off = -1e30f;
-    if constexpr (S > 0) {
-      off = (float)kMhsaS - __half2float(a.s.in[a.s.row_in(b) + kOffMhsaLen]);
-      if (a.reduced) off = floorf(off / 2.0f);
-    }
-    const bool live = lane < TK;
-#pragma unroll
-    for (int i = 0; i < T; ++i) {
-      const float4* q4 = reinterpret_cast<const float4*>(qs + i * kDk);
-      float acc = 0.f;
-#pragma unroll
-      for (int c4 = 0; c4 < kDk / 4; ++c4) {
-        const float4 q = q4[c4];
-        acc = fmaf(q.x, kr[4 * c4], acc);
-        acc = fmaf(q.y, kr[4 * c4 + 1], acc);
-        acc = fmaf(q.z, kr[4 * c4 + 2], acc);
-        acc = fmaf(q.w, kr[4 * c4 + 3], acc);
-      }
-      const float sc = acc / 6.928203230275509f;       // / math.sqrt(48) (submodules.py:185)
-      const bool masked = (S > 0) && (((float)lane < off) || ((float)(S + i) < off));
-      const float x = live ? (masked ? -10000.0f : sc) : -INFINITY;
-      const float m = wave_max(x);
-      const float e = live ? expf(x - m) : 0.f;
-      const float sum = wave_sum(e);
-      const float p = masked ? 0.f : e / sum;
-      if (live) {
-        ps[i * TKP + lane] = p;
-        if (a.probs) a.probs[(((int64_t)b * kHeads + h) * T + i) * TK + lane] = p;
-      }
-    }
-  } else {
-    static_assert(S == 0, "shared probabilities only in layers without a cache");
-    const float* pp = a.probs + ((int64_t)b * kHeads + h) * T * TK;
-    for (int e = lane; e < T * TK; e += 64) ps[(e / TK) * TKP + e % TK] = pp[e];
-  }
+  const float* pp = a.probs + ((int64_t)b * kHeads + h) * T * TK;
+  for (int e = lane; e < T * TK; e += 64) ps[(e / TK) * TKP + e % TK] = pp[e];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -258,25 +168,202 @@ __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
   }
 }
 
+// Recomputing layers (0, 7, 14, 15) on the matrix pipe.  One wave per (stream, head) as above, but the lanes are
+// (row, dim group): lane l = 16 g + r holds the 12 dims {4g .. 4g+3, 16+4g .. 16+4g+3, 32+4g .. 32+4g+3} of row r of
+// a 16-row tile (three 4-element vector loads), which is at once
+//   * the LayerNorm layout: the row's sums closed by two lane exchanges (xor 16, xor 32); each RoPE pair (d, d + 16),
+//     d < 16, sits in one lane (elements m and m + 4);
+//   * the operand layout of v_mfma_f32_16x16x4_f32 (lane l: A[l & 15][l >> 4], B[l >> 4][l & 15]): step m's k slot g
+//     is dim 16 (m >> 2) + 4 g + (m & 3) for both Q and K, so the 12 steps sum all 48 products (exact fp32 fmas; the
+//     order of the dims differs from a d-ordered chain, within the fp32 tolerance of the parity tests).
+// Scores are computed transposed, S^T = K Q^T (tile t: keys 16 t .. 16 t + 15), so a lane ends with keys
+// 16 t + 4 g + rr of query r: the softmax over keys is an in-lane reduction plus xor 16 / xor 32, and the
+// probabilities are already the A operand of ctx = P V (k slot g of step s <-> key 16 t + 4 g + s).  V goes to the
+// wave's LDS slice by LDS-DMA (4-8 instructions) and is read back in that order.  Every operand load is a vector
+// load: the texture-address unit processes a wave's 64 addresses per instruction, so 165 two-byte loads per wave cost
+// more than the arithmetic they replaced (measured 260 us at S + T = 40).  The round-3 kernel ran the 48-dim
+// LayerNorms and the dot products serially in T or S + T lanes of 64 (VALU-bound: 118-144 us per launch at B = 4096).
+template <int T, int S, bool OBF>
+__global__ void __launch_bounds__(256) attention_rec_kernel(AttnArgs a) {
+  constexpr int TK = S + T, NJT = (TK + 15) / 16;
+  constexpr int ES = OBF ? 2 : 4;                                   // bytes per activation element
+  constexpr int VPC = kDk * ES / 16;                                // 16-byte pieces per V row (6 | 12)
+  constexpr int VINS = (TK * VPC + 63) / 64;                        // LDS-DMA instructions per wave
+  static_assert(T <= 16, "one query tile");
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) uint8_t vs[4][VINS * 1024];
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int b = blockIdx.x >> 1, h = ((blockIdx.x & 1) << 2) + wid;
+  const int c0 = h * kDk, r16 = lane & 15, g = lane >> 4;
+  // V rows -> LDS (row j at j * 48 * ES bytes)
+#pragma unroll
+  for (int in = 0; in < VINS; ++in) {
+    const int pc = min(in * 64 + lane, TK * VPC - 1), j = pc / VPC, e = (pc % VPC) * (16 / ES);
+    const uint8_t* src = static_cast<const uint8_t*>(a.v) + (((int64_t)b * TK + j) * a.ldv + c0 + e) * ES;
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src, vs[wid] + in * 1024, 16, 0, 0);
+#else
+    (void)src;
+#endif
+  }
+  // Q and K rows, three 4-element loads per row
+  auto load_row = [&](const void* base, int64_t row, float (&x)[12]) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float4 v = load_act4<OBF>(base, row + c0 + 16 * ch + 4 * g);
+      x[4 * ch] = v.x; x[4 * ch + 1] = v.y; x[4 * ch + 2] = v.z; x[4 * ch + 3] = v.w;
+    }
+  };
+  float q[12], kk[NJT][12];
+  load_row(a.q, ((int64_t)b * T + min(r16, T - 1)) * a.ldq, q);
+#pragma unroll
+  for (int t = 0; t < NJT; ++t) load_row(a.k, ((int64_t)b * TK + min(16 * t + r16, TK - 1)) * a.ldk, kk[t]);
+  auto load_w = [&](const float* w, float (&x)[12]) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float4 v = *reinterpret_cast<const float4*>(w + 16 * ch + 4 * g);
+      x[4 * ch] = v.x; x[4 * ch + 1] = v.y; x[4 * ch + 2] = v.z; x[4 * ch + 3] = v.w;
+    }
+  };
+  // LayerNorm(48, eps 1e-5) + RoPE on dims [0, 32) of the row this lane's 12 dims belong to (pos = RoPE position)
+  auto ln_rope = [&](float (&x)[12], const float (&lw)[12], const float (&lb)[12], int pos) {
+    float sum = 0.f;
+#pragma unroll
+    for (int m = 0; m < 12; ++m) sum += x[m];
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float mu = sum * (1.0f / kDk);
+    float var = 0.f;
+#pragma unroll
+    for (int m = 0; m < 12; ++m) {
+      x[m] -= mu;
+      var += x[m] * x[m];
+    }
+    var += __shfl_xor(var, 16, 64);
+    var += __shfl_xor(var, 32, 64);
+    const float rstd = 1.0f / sqrtf(var * (1.0f / kDk) + kLnEps);
+#pragma unroll
+    for (int m = 0; m < 12; ++m) x[m] = x[m] * rstd * lw[m] + lb[m];
+    const float4 cs = *reinterpret_cast<const float4*>(a.rope_cos + (pos + kMhsaS) * (kRope / 2) + 4 * g);
+    const float4 sn = *reinterpret_cast<const float4*>(a.rope_sin + (pos + kMhsaS) * (kRope / 2) + 4 * g);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {                       // rotate_half pairs (d, d + 16), submodules.py:142-157
+      const float y0 = x[m], y1 = x[m + 4];
+      x[m] = y0 * cs[m] - y1 * sn[m];
+      x[m + 4] = y1 * cs[m] + y0 * sn[m];
+    }
+  };
+  {
+    float lw[12], lb[12];
+    load_w(a.qln_w, lw);
+    load_w(a.qln_b, lb);
+    ln_rope(q, lw, lb, min(r16, T - 1));
+  }
+  f32x4 st[NJT];
+  {
+    float lw[12], lb[12];
+    load_w(a.kln_w, lw);
+    load_w(a.kln_b, lb);
+#pragma unroll
+    for (int t = 0; t < NJT; ++t) {
+      ln_rope(kk[t], lw, lb, min(16 * t + r16, TK - 1) - S);
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < 12; ++m) st[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[t][m], q[m], st[t], 0, 0, 0);
+    }
+  }
+  // softmax over the keys of query i = r16 (this lane: keys 16 t + 4 g + rr)
+  float off = -1e30f;
+  if constexpr (S > 0) {
+    off = (float)kMhsaS - __half2float(a.s.in[a.s.row_in(b) + kOffMhsaLen]);
+    if (a.reduced) off = floorf(off / 2.0f);
+  }
+  const int i = r16;
+  float x[NJT][4];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < NJT; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int j = 16 * t + 4 * g + rr;
+      const float sc = st[t][rr] * 0.14433756729740643f;  // / math.sqrt(48) (submodules.py:185), as a product
+      const bool masked = (S > 0) && (((float)j < off) || ((float)(S + i) < off));
+      x[t][rr] = j < TK ? (masked ? -10000.0f : sc) : -INFINITY;
+      mx = fmaxf(mx, x[t][rr]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < NJT; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int j = 16 * t + 4 * g + rr;
+      x[t][rr] = j < TK ? expf(x[t][rr] - mx) : 0.f;
+      sum += x[t][rr];
+    }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float rsum = 1.0f / sum;                        // one division per lane, not one per probability
+  float* pr = a.probs ? a.probs + (((int64_t)b * kHeads + h) * T + i) * TK : nullptr;
+#pragma unroll
+  for (int t = 0; t < NJT; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int j = 16 * t + 4 * g + rr;
+      const bool masked = (S > 0) && (((float)j < off) || ((float)(S + i) < off));
+      x[t][rr] = masked ? 0.f : x[t][rr] * rsum;
+      if (pr && i < T && j < TK) pr[j] = x[t][rr];
+    }
+  // ctx = P V: D[query][column], lane: queries 4 g + rr, column 16 ct + r16; V from the LDS slice
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                 // the V DMA (this wave's own)
+  const uint8_t* vb = vs[wid];
+  f32x4 cx[3];
+#pragma unroll
+  for (int ct = 0; ct < 3; ++ct) cx[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NJT; ++t)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int j = min(16 * t + 4 * g + s4, TK - 1);
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) {
+        const int e = j * kDk + 16 * ct + r16;
+        float v;
+        if constexpr (OBF) v = __builtin_bit_cast(float, (uint32_t)(*reinterpret_cast<const uint16_t*>(vb + 2 * e)) << 16);
+        else v = *reinterpret_cast<const float*>(vb + 4 * e);
+        cx[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[t][s4], v, cx[ct], 0, 0, 0);
+      }
+    }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int iq = 4 * g + rr;
+    if (iq < T) {
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) store_act<OBF>(a.ctx, ((int64_t)b * T + iq) * kD + c0 + 16 * ct + r16, cx[ct][rr]);
+    }
+  }
+}
+
 template <bool OBF>
 static hipError_t launch_attention_t(const AttnArgs& a, hipStream_t st) {
   const dim3 grid(a.B * 2), block(256);
   // (T, S) of the 300 ms chunk: (10 | 5, 0), layer 14 (5, 15), layer 15 (10, 30); 400 ms: T 13 | 6
   if (!a.recompute) {
     if (a.S != 0) return hipErrorInvalidValue;
-    if (a.T == 10) hipLaunchKernelGGL((attention_kernel<10, 0, false, OBF>), grid, block, 0, st, a);
-    else if (a.T == 5) hipLaunchKernelGGL((attention_kernel<5, 0, false, OBF>), grid, block, 0, st, a);
-    else if (a.T == 13) hipLaunchKernelGGL((attention_kernel<13, 0, false, OBF>), grid, block, 0, st, a);
-    else if (a.T == 6) hipLaunchKernelGGL((attention_kernel<6, 0, false, OBF>), grid, block, 0, st, a);
+    if (a.T == 10) hipLaunchKernelGGL((attention_kernel<10, OBF>), grid, block, 0, st, a);
+    else if (a.T == 5) hipLaunchKernelGGL((attention_kernel<5, OBF>), grid, block, 0, st, a);
+    else if (a.T == 13) hipLaunchKernelGGL((attention_kernel<13, OBF>), grid, block, 0, st, a);
+    else if (a.T == 6) hipLaunchKernelGGL((attention_kernel<6, OBF>), grid, block, 0, st, a);
     else return hipErrorInvalidValue;
-  } else if (a.T == 10 && a.S == 0) hipLaunchKernelGGL((attention_kernel<10, 0, true, OBF>), grid, block, 0, st, a);
-  else if (a.T == 5 && a.S == 0) hipLaunchKernelGGL((attention_kernel<5, 0, true, OBF>), grid, block, 0, st, a);
-  else if (a.T == 5 && a.S == 15) hipLaunchKernelGGL((attention_kernel<5, 15, true, OBF>), grid, block, 0, st, a);
-  else if (a.T == 10 && a.S == 30) hipLaunchKernelGGL((attention_kernel<10, 30, true, OBF>), grid, block, 0, st, a);
-  else if (a.T == 13 && a.S == 0) hipLaunchKernelGGL((attention_kernel<13, 0, true, OBF>), grid, block, 0, st, a);
-  else if (a.T == 6 && a.S == 0) hipLaunchKernelGGL((attention_kernel<6, 0, true, OBF>), grid, block, 0, st, a);
-  else if (a.T == 6 && a.S == 15) hipLaunchKernelGGL((attention_kernel<6, 15, true, OBF>), grid, block, 0, st, a);
-  else if (a.T == 13 && a.S == 30) hipLaunchKernelGGL((attention_kernel<13, 30, true, OBF>), grid, block, 0, st, a);
+  } else if (a.T == 10 && a.S == 0) hipLaunchKernelGGL((attention_rec_kernel<10, 0, OBF>), grid, block, 0, st, a);
+  else if (a.T == 5 && a.S == 0) hipLaunchKernelGGL((attention_rec_kernel<5, 0, OBF>), grid, block, 0, st, a);
+  else if (a.T == 5 && a.S == 15) hipLaunchKernelGGL((attention_rec_kernel<5, 15, OBF>), grid, block, 0, st, a);
+  else if (a.T == 10 && a.S == 30) hipLaunchKernelGGL((attention_rec_kernel<10, 30, OBF>), grid, block, 0, st, a);
+  else if (a.T == 13 && a.S == 0) hipLaunchKernelGGL((attention_rec_kernel<13, 0, OBF>), grid, block, 0, st, a);
+  else if (a.T == 6 && a.S == 0) hipLaunchKernelGGL((attention_rec_kernel<6, 0, OBF>), grid, block, 0, st, a);
+  else if (a.T == 6 && a.S == 15) hipLaunchKernelGGL((attention_rec_kernel<6, 15, OBF>), grid, block, 0, st, a);
+  else if (a.T == 13 && a.S == 30) hipLaunchKernelGGL((attention_rec_kernel<13, 30, OBF>), grid, block, 0, st, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
