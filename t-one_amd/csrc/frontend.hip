@@ -318,54 +318,14 @@ constexpr int kC2Stages = (kC2Taps + kC2TP - 1) / kC2TP;  // 31
 
 __host__ __device__ __forceinline__ int c2_swz(int q) { return ((q >> 2) & 1) << 1; }
 
-__global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restrict__ x2, const uint16_t* __restrict__ w2c,
-                                                         const float* __restrict__ scale, const float* __restrict__ shift,
-                                                         uint16_t* __restrict__ flat) {
+// The 121-tap loop + BatchNorm/SiLU epilogue of conv2 over a slab already in LDS (ring first, then the slab, as
+// conv2_bf16_kernel lays them out); stage_taps(sg) issues stage sg's weight DMA; stages 0 and 1 are in flight.
+template <typename StageFn>
+__device__ __forceinline__ void conv2_taps(const float* lds, const float* sc, const float* sh, StageFn&& stage_taps,
+                                           uint16_t* __restrict__ flat, int b, int wid, int lane) {
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
   typedef float f32x4 __attribute__((ext_vector_type(4)));
-  // ONE LDS object: 3 ring slots | slab | scale | shift.  The ring comes first so that every fragment read of the
-  // unrolled tap loop is a per-lane VGPR base plus a compile-time immediate below 64 KiB: the ring slot and tap
-  // (slot * 16 KiB + u * 4 KiB) for the weights, the tap's input offset toff * 64 B for the slab.
-  __shared__ __attribute__((aligned(16))) float lds[3 * kC2Ring + kC2Slab + 2 * kSub2C];
-  float* ring = lds;
-  float* slab = lds + 3 * kC2Ring;
-  float* sc = slab + kC2Slab;
-  float* sh = sc + kSub2C;
   const char* lb = reinterpret_cast<const char*>(lds);
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint16_t* xb = x2 + (int64_t)b * kC2In * kSub1C;
-  if (tid < kSub2C) {
-    sc[tid] = scale[tid];
-    sh[tid] = shift[tid];
-  }
-  __syncthreads();                                        // before any LDS-DMA is in flight
-
-  auto stage_taps = [&](int sg) {                         // taps 4 sg .. 4 sg + 3: 16 pieces, 2 per wave
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int pc = wid * 2 + h, tap = min(sg * kC2TP + (pc >> 2), kC2Taps);   // past the end: the zero tap
-      const int L = (pc & 3) * 64 + lane, c = L >> 2, s = L & 3;
-      const uint16_t* src = w2c + (int64_t)c * kConv2KPad + tap * kSub1C + ((s ^ c2_swz(c)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, ring + (sg % 3) * kC2Ring + pc * 256, 16, 0, 0);
-#else
-      (void)src;
-      (void)ring;
-#endif
-    }
-  };
-  for (int pc = wid; pc < kC2SlabPieces; pc += 8) {       // the stream's input, once
-    const int L = pc * 64 + lane, q = min(L >> 2, kC2In - 1), s = L & 3;
-    const uint16_t* src = xb + q * kSub1C + ((s ^ c2_swz(q)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src, slab + pc * 256, 16, 0, 0);
-#else
-    (void)src;
-#endif
-  }
-  stage_taps(0);
-  stage_taps(1);
-
   // Per-lane byte offsets, computed once.  Slab position q = qb + toff (qb: the lane's output position's first input
   // position, toff = kt * 44 + kf: the tap) is read at q * 64 B + 16 B * (g ^ swz(q)); swz depends on bit 2 of q only,
   // i.e. on (qb + (toff & 7)) & 4, so xa[i][c] holds the offset for toff & 7 == c and the tap adds toff * 64 B as an
@@ -438,6 +398,239 @@ __global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restr
       *reinterpret_cast<uint2*>(dst + 16 * c + 4 * g) = make_uint2(lo, hi);
     }
   }
+}
+
+__global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restrict__ x2, const uint16_t* __restrict__ w2c,
+                                                         const float* __restrict__ scale, const float* __restrict__ shift,
+                                                         uint16_t* __restrict__ flat) {
+  // ONE LDS object: 3 ring slots | slab | scale | shift.  The ring comes first so that every fragment read of the
+  // unrolled tap loop is a per-lane VGPR base plus a compile-time immediate below 64 KiB: the ring slot and tap
+  // (slot * 16 KiB + u * 4 KiB) for the weights, the tap's input offset toff * 64 B for the slab.
+  __shared__ __attribute__((aligned(16))) float lds[3 * kC2Ring + kC2Slab + 2 * kSub2C];
+  float* ring = lds;
+  float* slab = lds + 3 * kC2Ring;
+  float* sc = slab + kC2Slab;
+  float* sh = sc + kSub2C;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint16_t* xb = x2 + (int64_t)b * kC2In * kSub1C;
+  if (tid < kSub2C) {
+    sc[tid] = scale[tid];
+    sh[tid] = shift[tid];
+  }
+  __syncthreads();                                        // before any LDS-DMA is in flight
+
+  auto stage_taps = [&](int sg) {                         // taps 4 sg .. 4 sg + 3: 16 pieces, 2 per wave
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pc = wid * 2 + h, tap = min(sg * kC2TP + (pc >> 2), kC2Taps);   // past the end: the zero tap
+      const int L = (pc & 3) * 64 + lane, c = L >> 2, s = L & 3;
+      const uint16_t* src = w2c + (int64_t)c * kConv2KPad + tap * kSub1C + ((s ^ c2_swz(c)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, ring + (sg % 3) * kC2Ring + pc * 256, 16, 0, 0);
+#else
+      (void)src;
+      (void)ring;
+#endif
+    }
+  };
+  for (int pc = wid; pc < kC2SlabPieces; pc += 8) {       // the stream's input, once
+    const int L = pc * 64 + lane, q = min(L >> 2, kC2In - 1), s = L & 3;
+    const uint16_t* src = xb + q * kSub1C + ((s ^ c2_swz(q)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src, slab + pc * 256, 16, 0, 0);
+#else
+    (void)src;
+#endif
+  }
+  stage_taps(0);
+  stage_taps(1);
+
+  conv2_taps(lds, sc, sh, stage_taps, flat, b, wid, lane);
+}
+
+// a3 in bf16 mode at 300 ms, fused: the pre-encode RMSNorm + conv1 (sub1_bf16_kernel's arithmetic) write the
+// conv2 input rows straight into this workgroup's LDS slab, so the 107 KB per stream of x2 is never written to HBM and
+// read back (sub1_bf16 + conv2_bf16: 287 + 598 us at B = 4096).  Phases of one workgroup (one stream):
+//   1. conv2 stage 0's weights DMA'd into ring slot 0 (in flight throughout);
+//   2. x1 = [sub1 state (10 rows) ; RMSNorm(feats) (30 rows)] (a wave per row, a lane per mel; the new sub1 state
+//      rows go out as fp16) -> four shifted bf16 copies in ring slots 1-2 (copy s holds x1[r][j + s], so an A fragment
+//      of 8 columns starting at any a is two 8-byte reads at column a - (a & 3));
+//   3. the sub2 state (fp16 [c][8][44]) -> slab rows 0..7 as 16-byte channel chunks;
+//   4. conv1 as sub1_bf16_kernel's Toeplitz MFMA (90 tiles of 16 positions x 32 channels over 8 waves, the weight
+//      fragments in registers), BN + SiLU, bf16 into slab rows 8..37 (the swizzled layout conv2 reads) and fp16 into
+//      the new sub2 state (rows 22..29);
+//   5. ring slots 1-2 are free again: stage 1's DMA, then conv2_taps as in conv2_bf16_kernel.
+constexpr int kF1Rows = kSub1S + 30;                 // x1 rows at 300 ms: 10 carried + 30 new
+constexpr int kF1Copy = kF1Rows * kX1Cols + 16;      // halves per shifted copy
+static_assert(4 * kF1Copy * 2 <= 2 * kC2Ring * 4, "four shifted copies fit in ring slots 1-2");
+
+__global__ void __launch_bounds__(512) sub_conv_bf16_kernel(const float* __restrict__ feats, StateRef s,
+                                                            const float* __restrict__ pre_norm_w,
+                                                            const uint16_t* __restrict__ w1t,
+                                                            const float* __restrict__ scale1,
+                                                            const float* __restrict__ shift1,
+                                                            const uint16_t* __restrict__ w2c,
+                                                            const float* __restrict__ scale2,
+                                                            const float* __restrict__ shift2,
+                                                            uint16_t* __restrict__ flat) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int kMT = 30;                            // mel frames (300 ms)
+  __shared__ __attribute__((aligned(16))) float lds[3 * kC2Ring + kC2Slab + 2 * kSub2C + 2 * kSub1C];
+  float* ring = lds;
+  float* slab = lds + 3 * kC2Ring;
+  float* sc = slab + kC2Slab;
+  float* sh = sc + kSub2C;
+  float* sc1 = sh + kSub2C;
+  float* sh1 = sc1 + kSub1C;
+  uint16_t* xc = reinterpret_cast<uint16_t*>(ring + kC2Ring);
+  uint16_t* slab16 = reinterpret_cast<uint16_t*>(slab);
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t srow = s.row_in(b), orow = s.row_out(b);
+  if (tid < kSub2C) {
+    sc[tid] = scale2[tid];
+    sh[tid] = shift2[tid];
+  }
+  if (tid < kSub1C) {
+    sc1[tid] = scale1[tid];
+    sh1[tid] = shift1[tid];
+  }
+  __syncthreads();                                        // before any LDS-DMA is in flight
+
+  auto stage_taps = [&](int sg) {                         // taps 4 sg .. 4 sg + 3: 16 pieces, 2 per wave
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pc = wid * 2 + h, tap = min(sg * kC2TP + (pc >> 2), kC2Taps);   // past the end: the zero tap
+      const int L = (pc & 3) * 64 + lane, c = L >> 2, q = L & 3;
+      const uint16_t* src = w2c + (int64_t)c * kConv2KPad + tap * kSub1C + ((q ^ c2_swz(c)) << 3);
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_amdgcn_global_load_lds(src, ring + (sg % 3) * kC2Ring + pc * 256, 16, 0, 0);
+#else
+      (void)src;
+      (void)ring;
+#endif
+    }
+  };
+  stage_taps(0);
+
+  // conv1 weight fragments: B operand lane (n = lane & 15, k group g = lane >> 4): w1t[kt][16 nt + n][8 g .. 8 g + 7]
+  const int g = lane >> 4, n = lane & 15;
+  bf16x8 wf[kSub1Kt][2];
+#pragma unroll
+  for (int kt = 0; kt < kSub1Kt; ++kt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      wf[kt][nt] = *reinterpret_cast<const bf16x8*>(w1t + ((kt * kSub1C + 16 * nt + n) * 32 + 8 * g));
+
+  // every global load of phases 2-3 is issued before any of their arithmetic (one memory round trip, not one per
+  // row: the first version, a loop of dependent row loads, spent as long in this phase as the separate sub1 launch)
+  constexpr int kRowsPerWave = kF1Rows / 8;               // 5
+  constexpr int kStItems = kSub2S * kSub1F * 4;           // 1408 (position, 8-channel chunk) items
+  constexpr int kStPerThread = (kStItems + 511) / 512;    // 3
+  static_assert(kF1Rows % 8 == 0, "x1 rows over 8 waves");
+  float xs[kRowsPerWave], xf[kRowsPerWave];
+#pragma unroll
+  for (int k = 0; k < kRowsPerWave; ++k) {
+    const int r = wid + 8 * k;
+    xs[k] = __half2float(s.in[srow + kOffSub1 + min(r, kSub1S - 1) * kMels + lane]);
+    xf[k] = feats[((int64_t)b * kMT + max(r - kSub1S, 0)) * kMels + lane];
+  }
+  const float pw = pre_norm_w[lane];
+  const __half* st2in = s.in + srow + kOffSub2;
+  __half sv[kStPerThread][8];
+#pragma unroll
+  for (int k = 0; k < kStPerThread; ++k) {
+    const int i = min(tid + 512 * k, kStItems - 1), q = i >> 2, ck = i & 3;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sv[k][e] = st2in[(8 * ck + e) * kSub2S * kSub1F + q];
+  }
+  // x1 rows -> the four shifted bf16 copies (copy q, row r, column j: x1[r][j + q], zero past the row)
+#pragma unroll
+  for (int k = 0; k < kRowsPerWave; ++k) {
+    const int r = wid + 8 * k;
+    float y;
+    if (r < kSub1S) {
+      y = xs[k];
+    } else {
+      const int t = r - kSub1S;
+      const float v = xf[k];
+      const float ssq = wave_sum(v * v);
+      const float rms = sqrtf(ssq) * 0.125f;
+      y = pw * (v / (rms + kRmsEps));
+      if (t >= kMT - kSub1S) s.out[orow + kOffSub1 + (t - (kMT - kSub1S)) * kMels + lane] = __float2half_rn(y);
+    }
+    const __bf16 hy = (__bf16)y;
+    const uint16_t hb = __builtin_bit_cast(uint16_t, hy);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint16_t* row = xc + q * kF1Copy + r * kX1Cols;
+      if (lane >= q) row[lane - q] = hb;
+      if (lane < 16 + q) row[kMels - q + lane] = 0;
+    }
+  }
+  // carried conv2-input rows (sub2 state [c][8][44], fp16) -> slab rows 0..7: 16-byte chunks of 8 channels
+#pragma unroll
+  for (int k = 0; k < kStPerThread; ++k) {
+    const int i = tid + 512 * k, q = i >> 2, ck = i & 3;
+    if (i < kStItems) {
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 lo = (__bf16)__half2float(sv[k][2 * e]);
+        const __bf16 hi = (__bf16)__half2float(sv[k][2 * e + 1]);
+        w[e] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+      }
+      *reinterpret_cast<uint4*>(slab16 + q * kSub1C + ((ck ^ c2_swz(q)) << 3)) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  __syncthreads();
+
+  // conv1 tiles -> slab rows 8..37 (and the new sub2 state)
+  __half* st2out = s.out + orow + kOffSub2;
+  for (int tile = wid; tile < kMT * 3; tile += 8) {
+    const int t = tile / 3, f0 = (tile % 3) * 16;
+    const int a = f0 + n + 8 * g, q = a & 3;                 // A operand: position f0 + n, k group g
+    const uint16_t* arow = xc + q * kF1Copy + t * kX1Cols + (a - q);
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kt = 0; kt < kSub1Kt; ++kt) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(arow + kt * kX1Cols);
+      const uint2 hi = *reinterpret_cast<const uint2*>(arow + kt * kX1Cols + 4);
+      const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wf[kt][0], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wf[kt][1], acc[1], 0, 0, 0);
+    }
+    // D 16x16: lane holds channel 16 nt + n of positions f0 + 4 g + r
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int c = 16 * nt + n;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = f0 + 4 * g + r;
+        const float z = fmaf(acc[nt][r], sc1[c], sh1[c]);   // SiLU via v_exp_f32 / v_rcp_f32 (bf16 output)
+        const float y = z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
+        if (f < kSub1F) {
+          const int p = (kSub2S + t) * kSub1F + f;
+          const __bf16 hy = (__bf16)y;
+          slab16[p * kSub1C + (((c >> 3) ^ c2_swz(p)) << 3) + (c & 7)] = __builtin_bit_cast(uint16_t, hy);
+          if (t >= kMT - kSub2S) st2out[(c * kSub2S + (t - (kMT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
+        }
+      }
+    }
+  }
+  __syncthreads();                                        // the slab is complete; ring slots 1-2 are free
+  stage_taps(1);
+  conv2_taps(lds, sc, sh, stage_taps, flat, b, wid, lane);
+}
+
+hipError_t launch_sub_conv_bf16(const float* feats, StateRef s, const float* pre_norm_w, const void* w1t,
+                                const float* scale1, const float* shift1, const void* w2c, const float* scale2,
+                                const float* shift2, void* flat, int B, hipStream_t st) {
+  if (!w1t) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sub_conv_bf16_kernel, dim3(B), dim3(512), 0, st, feats, s, pre_norm_w,
+                     static_cast<const uint16_t*>(w1t), scale1, shift1, static_cast<const uint16_t*>(w2c), scale2,
+                     shift2, static_cast<uint16_t*>(flat));
+  return hipGetLastError();
 }
 
 hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale, const float* shift, void* flat, int B,

@@ -138,6 +138,10 @@ hipError_t conv2_gemm(const void* x2, const void* w, const float* scale, const f
 
 // a3 conv2 in bf16 mode, one workgroup per stream over an LDS-resident input slab (frontend.hip);
 // x2 bf16 [B][38][44][32], w2c bf16 [64][3904] tap-major, flat bf16 [B*10][34*64]
+// a3 in bf16 mode at 300 ms: pre-encode RMSNorm + conv1 + conv2 in one launch (the conv2 input stays in LDS)
+hipError_t launch_sub_conv_bf16(const float* feats, StateRef s, const float* pre_norm_w, const void* w1t,
+                                const float* scale1, const float* shift1, const void* w2c, const float* scale2,
+                                const float* shift2, void* flat, int B, hipStream_t st);
 hipError_t launch_conv2_bf16(const void* x2, const void* w2c, const float* scale, const float* shift, void* flat, int B,
                              hipStream_t st);
 // a3 conv2 in fp32 (split) mode, input rows split once per kernel row (frontend.hip conv2_p3_kernel);

@@ -497,9 +497,14 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
   LAUNCH("mel_prep", launch_mel_prep(signal, sr, s->wave, B, geo.chunk, st));
   LAUNCH("mel", mel_gemms(s->wave, s->basis_p, s->fbank_p, s->power, s->feats, B, geo.chunk, st));
   if (s->debug_stop == 0) return TONE_OK;
-  LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B, geo.chunk,
-                             st));
-  LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, geo.chunk, s->w2p));
+  if (bf && geo.T == kT) {   // 300 ms bf16 / fp8: conv1 output straight into conv2's LDS slab
+    LAUNCH("sub_conv", launch_sub_conv_bf16(s->feats, sr, s->pre_norm, s->w1t, s->scale1, s->shift1, s->w2c, s->scale2,
+                                            s->shift2, s->flat, B, st));
+  } else {
+    LAUNCH("sub1", launch_sub1(s->feats, sr, s->pre_norm, s->w1, s->w1t, s->scale1, s->shift1, s->x2, bf, B,
+                               geo.chunk, st));
+    LAUNCH("conv2", conv2_gemm(s->x2, s->w2c, s->scale2, s->shift2, s->flat, B, bf, st, geo.chunk, s->w2p));
+  }
   CALL(gemm_call(s, st, "gemm_sub_out", s->flat, kSubOut, s->wsub_out, s->rA, D, nullptr, B * geo.T, D, kSubOut,
                  EPI_STORE, 0, nullptr, 1.0f, /*a_bf16=*/true));
   // fp8 mode: the norms that feed a layer's FFN1 directly, FFN1's down-projection (before q|k|v) and pw2 (before FFN2)
