@@ -432,7 +432,12 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g,
       float acc = bb;
 #pragma unroll
       for (int k = 0; k < kConvK; ++k) acc = fmaf(wr[k], x[t + k], acc);
-      store_act<OBF>(out, ((int64_t)b * T + t) * kD + ch, silu_f(acc));
+      // bf16 output: SiLU on v_exp_f32 / v_rcp_f32 as the conv epilogues (a few ulp of fp32 before the bf16
+      // rounding; the IEEE expf + division was a third of the kernel's VALU); fp32 output: IEEE exp / division
+      float y;
+      if constexpr (OBF) y = acc * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc * -1.4426950408889634f));
+      else y = silu_f(acc);
+      store_act<OBF>(out, ((int64_t)b * T + t) * kD + ch, y);
     }
 #pragma unroll
     for (int i = 0; i < kConvS; ++i) h[i] = __float2half_rn(x[T + i]);
