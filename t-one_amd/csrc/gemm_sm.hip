@@ -23,12 +23,17 @@
 namespace tone {
 namespace {
 
-template <int EPI, int MB, int KS, int STEPS, bool RS>
+//   * DWT > 0 (EPI_GLU, the conv module's pointwise-1 at T = DWT frames per stream): the 16 GLU output channels of
+//     all M rows go through LDS to one lane per (stream, channel), which runs dwconv_kernel's depthwise conv over
+//     [conv state ; the stream's T rows] (same taps, same fma order, IEEE SiLU) and writes the next state: the
+//     separate dwconv launch (5 us at B = 1) is gone.  Its taps and state are loaded before the K loop.
+template <int EPI, int MB, int KS, int STEPS, bool RS, int DWT = 0>
 __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
   constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
   constexpr int NB = PAIRED ? 2 : 1;
   constexpr int RED = (KS - 1) * NB * MB * 4 * 64;                 // K-split partial sums (floats)
   constexpr int REDS = RS ? (KS - 1) * MB * 64 : 0;                // ... and row sums of squares
+  static_assert(DWT == 0 || (EPI == EPI_GLU && RED >= MB * 16 * 16), "dwconv fusion: GLU, the tile fits in LDS");
   __shared__ __attribute__((aligned(16))) float lds[(RED > 0 ? RED : 1) + (REDS > 0 ? REDS : 1)];
 
   const int tid = threadIdx.x, lane = tid & 63, wk = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -62,6 +67,19 @@ __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
   const float* xr[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) xr[mb] = X + (int64_t)min(16 * mb + l16, p.M - 1) * p.lda + kb + 4 * lg;
+
+  // dwconv operands of the lane's first (stream, channel) pair, loaded under the W stream
+  constexpr int DT = DWT > 0 ? DWT : 1;
+  float dwk[DWT > 0 ? kConvK : 1], dwx[DWT > 0 ? kConvS : 1], dwb = 0.f;
+  if constexpr (DWT > 0) {
+    const int ch = c0 + (lane & 15), b = min(lane >> 4, p.M / DT - 1);
+#pragma unroll
+    for (int k = 0; k < kConvK; ++k) dwk[k] = p.dw.w[k * kD + ch];
+    dwb = p.dw.b[ch];
+    const __half* st = p.dw.s.in + p.dw.s.row_in(b) + kOffConv + (int64_t)p.dw.layer * kD * kConvS + ch * kConvS;
+#pragma unroll
+    for (int i = 0; i < kConvS; ++i) dwx[i] = __half2float(st[i]);
+  }
 
 #pragma unroll
   for (int s = 0; s < STEPS; ++s) {
@@ -102,71 +120,120 @@ __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
       }
     }
     __syncthreads();
-    if (wk > 0) return;
+    if constexpr (DWT == 0) {
+      if (wk > 0) return;
+    }
+  }
+  // reduction + epilogue: wave 0 (with DWT the other waves wait for the GLU tile, then share the depthwise conv)
+  if (DWT == 0 || wk == 0) {
+    if constexpr (KS > 1) {
 #pragma unroll
-    for (int g = 1; g < KS; ++g) {
+      for (int g = 1; g < KS; ++g) {
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
+        for (int i = 0; i < NB; ++i)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(lds + ((((g - 1) * NB + i) * MB + mb) * 64 + lane) * 4);
-          acc[i][mb] += v;
+          for (int mb = 0; mb < MB; ++mb) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(lds + ((((g - 1) * NB + i) * MB + mb) * 64 + lane) * 4);
+            acc[i][mb] += v;
+          }
+        if constexpr (RS) {
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) ss[mb] += lds[RED + ((g - 1) * MB + mb) * 64 + lane];
         }
-      if constexpr (RS) {
+      }
+    }
+
+    // epilogue (wave 0): lane holds row m = 16 mb + l16, columns c0 + 4 lg .. + 3
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) ss[mb] += lds[RED + ((g - 1) * MB + mb) * 64 + lane];
+    for (int mb = 0; mb < MB; ++mb) {
+      float inv = 1.0f;
+      if constexpr (RS) {
+        float t = ss[mb] + __shfl_xor(ss[mb], 16, 64);
+        t += __shfl_xor(t, 32, 64);
+        inv = 1.0f / (sqrtf(t) * p.inv_sqrt_k + kRmsEps);
+      }
+      const int m = 16 * mb + l16;
+      if (m >= p.M) continue;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0[0] + 4 * lg + r;
+        const float bg = p.bias ? p.bias[n] : 0.f;
+        const float g = fmaf(acc[0][mb][r], inv, bg);
+        if constexpr (PAIRED) {
+          const float bu = p.bias ? p.bias[n0[NB - 1] + 4 * lg + r] : 0.f;
+          const float u = fmaf(acc[NB - 1][mb][r], inv, bu);
+          o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);
+        } else {
+          o[r] = g;
+        }
+      }
+      if constexpr (DWT > 0) {   // the GLU tile -> LDS (the partial sums there are consumed)
+        *reinterpret_cast<f32x4*>(lds + m * 16 + 4 * lg) = f32x4{o[0], o[1], o[2], o[3]};
+        continue;
+      }
+      float* crow = static_cast<float*>(p.C) + (int64_t)m * p.ldc + c0 + 4 * lg;
+      if constexpr (EPI == EPI_RESID) {
+        const f32x4 rr = *reinterpret_cast<const f32x4*>(p.R + (int64_t)m * p.ldr + c0 + 4 * lg);
+        *reinterpret_cast<f32x4*>(crow) = f32x4{rr.x + p.alpha * o[0], rr.y + p.alpha * o[1], rr.z + p.alpha * o[2],
+                                                rr.w + p.alpha * o[3]};
+      } else {
+        *reinterpret_cast<f32x4*>(crow) = f32x4{o[0], o[1], o[2], o[3]};
       }
     }
   }
-
-  // epilogue (wave 0): lane holds row m = 16 mb + l16, columns c0 + 4 lg .. + 3
+  if constexpr (DWT > 0) {
+    __syncthreads();                                     // the GLU tile is in LDS
+    const int nb = p.M / DT;
+    for (int pr = lane; pr < nb * 16; pr += 64) {
+      const int b = pr >> 4, cl = pr & 15, ch = c0 + cl;
+      const int64_t sec = kOffConv + (int64_t)p.dw.layer * kD * kConvS + ch * kConvS;
+      if (pr >= 64) {   // streams 4 and up (B > 4): their state now
+        const __half* st = p.dw.s.in + p.dw.s.row_in(b) + sec;
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    float inv = 1.0f;
-    if constexpr (RS) {
-      float t = ss[mb] + __shfl_xor(ss[mb], 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      inv = 1.0f / (sqrtf(t) * p.inv_sqrt_k + kRmsEps);
-    }
-    const int m = 16 * mb + l16;
-    if (m >= p.M) continue;
-    float o[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0[0] + 4 * lg + r;
-      const float bg = p.bias ? p.bias[n] : 0.f;
-      const float g = fmaf(acc[0][mb][r], inv, bg);
-      if constexpr (PAIRED) {
-        const float bu = p.bias ? p.bias[n0[NB - 1] + 4 * lg + r] : 0.f;
-        const float u = fmaf(acc[NB - 1][mb][r], inv, bu);
-        o[r] = (EPI == EPI_SWIGLU) ? silu_f(g) * u : g * sigmoid_f(u);
-      } else {
-        o[r] = g;
+        for (int i = 0; i < kConvS; ++i) dwx[i] = __half2float(st[i]);
       }
-    }
-    float* crow = static_cast<float*>(p.C) + (int64_t)m * p.ldc + c0 + 4 * lg;
-    if constexpr (EPI == EPI_RESID) {
-      const f32x4 rr = *reinterpret_cast<const f32x4*>(p.R + (int64_t)m * p.ldr + c0 + 4 * lg);
-      *reinterpret_cast<f32x4*>(crow) = f32x4{rr.x + p.alpha * o[0], rr.y + p.alpha * o[1], rr.z + p.alpha * o[2],
-                                              rr.w + p.alpha * o[3]};
-    } else {
-      *reinterpret_cast<f32x4*>(crow) = f32x4{o[0], o[1], o[2], o[3]};
+      float x[kConvS + DT];
+#pragma unroll
+      for (int i = 0; i < kConvS; ++i) x[i] = dwx[i];
+#pragma unroll
+      for (int t = 0; t < DT; ++t) x[kConvS + t] = lds[(b * DT + t) * 16 + cl];
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {                     // the KS waves take every KS-th output frame
+        if (t % KS != wk) continue;
+        float acc = dwb;
+#pragma unroll
+        for (int k = 0; k < kConvK; ++k) acc = fmaf(dwk[k], x[t + k], acc);
+        p.dw.out[((int64_t)b * DT + t) * kD + ch] = silu_f(acc);
+      }
+      __half* so = p.dw.s.out + p.dw.s.row_out(b) + sec;
+#pragma unroll
+      for (int i = 0; i < kConvS; ++i)
+        if (i % KS == wk) so[i] = __float2half_rn(x[DT + i]);
     }
   }
 }
 
-template <int EPI, int KS, int STEPS, bool RS>
+template <int EPI, int KS, int STEPS, bool RS, int DWT = 0>
 hipError_t launch_sm_mb(const GemmArgs& a, hipStream_t st) {
   constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
   const dim3 grid(PAIRED ? a.N / 32 : a.N / 16), block(KS * 64);
   switch ((a.M + 15) / 16) {
-    case 1: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 1, KS, STEPS, RS>), grid, block, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 2, KS, STEPS, RS>), grid, block, 0, st, a); break;
-    case 3: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 3, KS, STEPS, RS>), grid, block, 0, st, a); break;
-    case 4: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 4, KS, STEPS, RS>), grid, block, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 1, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 2, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 3, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 4, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// pointwise-1 (GLU, rowscale, K = 384) with the depthwise conv in the epilogue: frames per stream as a template
+// argument (the dwconv registers stay registers)
+template <int DWT>
+hipError_t launch_sm_dw(const GemmArgs& a, hipStream_t st) {
+  if (a.M % DWT || a.N != 2 * kD) return hipErrorInvalidValue;
+  return launch_sm_mb<EPI_GLU, 4, 6, true, DWT>(a, st);
 }
 
 }  // namespace
@@ -180,6 +247,16 @@ hipError_t gemm_sm(const GemmArgs& a, int epi, hipStream_t st) {
   const bool paired = (epi == EPI_SWIGLU || epi == EPI_GLU);
   if (a.N % (paired ? 64 : 16)) return hipErrorInvalidValue;
   const bool rs = a.rowscale != 0;
+  if (a.dw.w) {
+    if (epi != EPI_GLU || a.K != 384 || !rs || !a.dw.out) return hipErrorInvalidValue;
+    switch (a.dw.T) {
+      case 10: return launch_sm_dw<10>(a, st);
+      case 5: return launch_sm_dw<5>(a, st);
+      case 13: return launch_sm_dw<13>(a, st);
+      case 6: return launch_sm_dw<6>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (a.K == 384) {
     switch (epi) {
       case EPI_STORE: return rs ? launch_sm_mb<EPI_STORE, 4, 6, true>(a, st) : launch_sm_mb<EPI_STORE, 4, 6, false>(a, st);

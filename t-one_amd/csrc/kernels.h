@@ -18,6 +18,16 @@ const Knobs& knobs();
 
 enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GLU = 3, EPI_CONV2 = 4, EPI_POWER = 5, EPI_LOGMEL = 6 };
 
+// fp32 mode, M <= 64 (gemm_sm): the depthwise conv module part (dwconv_kernel's arithmetic, bit for bit) run in the
+// GLU projection's epilogue, so the pointwise-1 output never leaves the workgroup; w == nullptr: off
+struct DwFuse {
+  const float* w;     // [31][384] folded taps
+  const float* b;     // [384] folded bias
+  StateRef s;         // conv state section of layer `layer`
+  int layer;
+  int T;              // frames per stream (M = streams x T)
+  float* out;         // [M][384] SiLU output (pw2's A)
+};
 struct GemmArgs {
   const void* A;      // [M][K] fp32, or bf16 bits when a_bf16
   int64_t lda;
@@ -57,6 +67,7 @@ struct GemmArgs {
   int conv_t, conv_in; // EPI_CONV2: frames per chunk and conv2 input rows per stream (chunk geometry, common.h Geom)
   int res16;          // bf16 / fp8 modes: the residual stream is fp16 -- RESID reads R and writes C as fp16, STORE
                       // writes C as fp16 (the shadow C2 stays bf16)
+  DwFuse dw;          // EPI_GLU on gemm_sm only: the depthwise conv in the epilogue (C is not written)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);

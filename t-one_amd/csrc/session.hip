@@ -391,8 +391,9 @@ struct Scope {
 int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, int64_t lda, const void* W, void* C,
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
               float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr,
-              bool mx_out = false) {
+              bool mx_out = false, const DwFuse* dw = nullptr) {
   GemmArgs a{};   // value-initialised: every field not set below is zero
+  if (dw) a.dw = *dw;
   a.A = A;
   a.lda = lda;
   a.W = W;
@@ -613,9 +614,16 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
     q8_fresh = false;
     // Convolution module (conformer_blocks.py:827-830)
-    CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true,
-                   true));   // g in bf16 in the bf16 / fp8 modes (fp32 in fp32 mode: gemm_call drops c_bf16 there)
-    LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st));
+    // fp32 mode at M <= 64 (the drop-in's per-call batch): the depthwise conv runs in pw1's epilogue (gemm_sm.hip)
+    if (s->precision == TONE_PRECISION_FP32 && M <= 64 && s->w3.count(w.wpw1)) {
+      const DwFuse dw{w.wdw, w.bdw, sr, l, T, static_cast<float*>(s->d)};
+      CALL(gemm_call(s, st, "gemm_pw1_dwconv", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f,
+                     false, false, nullptr, false, &dw));
+    } else {
+      CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true,
+                     true));   // g in bf16 in the bf16 / fp8 modes (fp32 in fp32 mode: gemm_call drops c_bf16 there)
+      LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st));
+    }
     // fp8 mode: pw2 also emits FFN2's MXFP8 operand
     CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs, f8n));
     q8_fresh = f8n;
