@@ -990,6 +990,7 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   const int bk = bf16 ? 64 : 32;
   // the depthwise conv in the GLU epilogue exists on gemm_sm only (fp32 mode, M <= 64): no other route
   if (a.dw.w) return (!bf16 && epi == EPI_GLU && a.M <= 64) ? gemm_sm(a, epi, st) : hipErrorInvalidValue;
+  if (a.att.probs) return (!bf16 && epi == EPI_RESID && a.M <= 64) ? gemm_sm(a, epi, st) : hipErrorInvalidValue;
   // the fp16 residual stream exists in the bf16 / fp8 modes only (the LDS-DMA and f32t kernels of gemm_bf16)
   if (a.res16 && (!bf16 || !a.a_bf16 || a.c_bf16 || (epi != EPI_STORE && epi != EPI_RESID))) return hipErrorInvalidValue;
   if (bf16 && a.a_bf16) {

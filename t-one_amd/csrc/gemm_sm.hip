@@ -27,7 +27,10 @@ namespace {
 //     all M rows go through LDS to one lane per (stream, channel), which runs dwconv_kernel's depthwise conv over
 //     [conv state ; the stream's T rows] (same taps, same fma order, IEEE SiLU) and writes the next state: the
 //     separate dwconv launch (5 us at B = 1) is gone.  Its taps and state are loaded before the K loop.
-template <int EPI, int MB, int KS, int STEPS, bool RS, int DWT = 0>
+//   * ATT > 0 (EPI_RESID, K = 384: the attn-out projection of a shared-probability layer at T = ATT frames): the A
+//     operand is ctx = P V, computed per 4-column fragment in the K loop (attention_kernel's j-ordered fma chain, so
+//     the same values) from the probabilities and V; the separate attention launch is gone.
+template <int EPI, int MB, int KS, int STEPS, bool RS, int DWT = 0, int ATT = 0>
 __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
   constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
   constexpr int NB = PAIRED ? 2 : 1;
@@ -87,7 +90,27 @@ __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) w[i] = *reinterpret_cast<const f32x4*>(wr[i] + 16 * s);
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) x[mb] = *reinterpret_cast<const f32x4*>(xr[mb] + 16 * s);
+    for (int mb = 0; mb < MB; ++mb) {
+      if constexpr (ATT > 0) {
+        const int m = min(16 * mb + l16, p.M - 1), sb = m / ATT, i = m - sb * ATT;
+        const int k0 = kb + 16 * s + 4 * lg, h = k0 / kDk;
+        const float* pr = p.att.probs + (((int64_t)sb * kHeads + h) * ATT + i) * ATT;
+        const float* vr = p.att.v + (int64_t)sb * ATT * p.att.ldv + k0;
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < ATT; ++j) {
+          const float pj = pr[j];
+          const f32x4 vj = *reinterpret_cast<const f32x4*>(vr + (int64_t)j * p.att.ldv);
+          c.x = fmaf(pj, vj.x, c.x);
+          c.y = fmaf(pj, vj.y, c.y);
+          c.z = fmaf(pj, vj.z, c.z);
+          c.w = fmaf(pj, vj.w, c.w);
+        }
+        x[mb] = c;
+      } else {
+        x[mb] = *reinterpret_cast<const f32x4*>(xr[mb] + 16 * s);
+      }
+    }
     if constexpr (RS) {
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
@@ -214,15 +237,15 @@ __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
   }
 }
 
-template <int EPI, int KS, int STEPS, bool RS, int DWT = 0>
+template <int EPI, int KS, int STEPS, bool RS, int DWT = 0, int ATT = 0>
 hipError_t launch_sm_mb(const GemmArgs& a, hipStream_t st) {
   constexpr bool PAIRED = (EPI == EPI_SWIGLU || EPI == EPI_GLU);
   const dim3 grid(PAIRED ? a.N / 32 : a.N / 16), block(KS * 64);
   switch ((a.M + 15) / 16) {
-    case 1: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 1, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 2, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
-    case 3: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 3, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
-    case 4: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 4, KS, STEPS, RS, DWT>), grid, block, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 1, KS, STEPS, RS, DWT, ATT>), grid, block, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 2, KS, STEPS, RS, DWT, ATT>), grid, block, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 3, KS, STEPS, RS, DWT, ATT>), grid, block, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((gemm_sm_kernel<EPI, 4, KS, STEPS, RS, DWT, ATT>), grid, block, 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -254,6 +277,16 @@ hipError_t gemm_sm(const GemmArgs& a, int epi, hipStream_t st) {
       case 5: return launch_sm_dw<5>(a, st);
       case 13: return launch_sm_dw<13>(a, st);
       case 6: return launch_sm_dw<6>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (a.att.probs) {   // attn-out of a shared-probability layer, ctx computed in the operand loads
+    if (epi != EPI_RESID || a.K != kD || rs || !a.att.v || a.att.ldv % 4 || a.M % a.att.T) return hipErrorInvalidValue;
+    switch (a.att.T) {
+      case 10: return launch_sm_mb<EPI_RESID, 4, 6, false, 0, 10>(a, st);
+      case 5: return launch_sm_mb<EPI_RESID, 4, 6, false, 0, 5>(a, st);
+      case 13: return launch_sm_mb<EPI_RESID, 4, 6, false, 0, 13>(a, st);
+      case 6: return launch_sm_mb<EPI_RESID, 4, 6, false, 0, 6>(a, st);
       default: return hipErrorInvalidValue;
     }
   }

@@ -28,6 +28,14 @@ struct DwFuse {
   int T;              // frames per stream (M = streams x T)
   float* out;         // [M][384] SiLU output (pw2's A)
 };
+// fp32 mode, M <= 64 (gemm_sm): a shared-probability attention layer's context (ctx = P V, attention_kernel's fma
+// order) computed in the attn-out projection's operand loads, so ctx never exists; probs == nullptr: off
+struct AttFuse {
+  const float* probs; // [B][8][T][T], the last recomputing layer's probabilities
+  const float* v;     // V rows b*T + j, ldv apart
+  int64_t ldv;
+  int T;
+};
 struct GemmArgs {
   const void* A;      // [M][K] fp32, or bf16 bits when a_bf16
   int64_t lda;
@@ -68,6 +76,7 @@ struct GemmArgs {
   int res16;          // bf16 / fp8 modes: the residual stream is fp16 -- RESID reads R and writes C as fp16, STORE
                       // writes C as fp16 (the shadow C2 stays bf16)
   DwFuse dw;          // EPI_GLU on gemm_sm only: the depthwise conv in the epilogue (C is not written)
+  AttFuse att;        // EPI_RESID, K = 384 on gemm_sm only: A = ctx computed from P and V (A is not read)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);

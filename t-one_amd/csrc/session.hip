@@ -391,9 +391,10 @@ struct Scope {
 int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, int64_t lda, const void* W, void* C,
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
               float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr,
-              bool mx_out = false, const DwFuse* dw = nullptr) {
+              bool mx_out = false, const DwFuse* dw = nullptr, const AttFuse* att = nullptr) {
   GemmArgs a{};   // value-initialised: every field not set below is zero
   if (dw) a.dw = *dw;
+  if (att) a.att = *att;
   a.A = A;
   a.lda = lda;
   a.W = W;
@@ -610,8 +611,16 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       aa.k = act_at(s->kvp, 0, bf); aa.ldk = 2 * D;
       aa.v = act_at(s->kvp, D, bf); aa.ldv = 2 * D;
     }
-    LAUNCH("attention", launch_attention(aa, st));
-    CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs));
+    // fp32 mode at M <= 64, shared-probability layers: ctx = P V inside the attn-out projection (gemm_sm.hip)
+    if (!aa.recompute && s->precision == TONE_PRECISION_FP32 && M <= 64 && s->w3.count(w.wo)) {
+      const AttFuse af{aa.probs, static_cast<const float*>(aa.v), aa.ldv, T};
+      CALL(gemm_call(s, st, "gemm_attn_out_ctx", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, false,
+                     false, nullptr, false, nullptr, &af));
+    } else {
+      LAUNCH("attention", launch_attention(aa, st));
+      CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false,
+                     xs));
+    }
     q8_fresh = false;
     // Convolution module (conformer_blocks.py:827-830)
     // fp32 mode at M <= 64 (the drop-in's per-call batch): the depthwise conv runs in pw1's epilogue (gemm_sm.hip)
