@@ -1126,9 +1126,9 @@ hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank
   m.ldc = kMels;
   m.n_out = kMels;
   m.M = B * geo.melT;
-  m.N = 128;
+  m.N = kMels;   // the 64 filter rows of the zero-padded [128][128] fbank (a 128-wide tile computed 64 zero columns)
   m.K = kMelPowCols;
-  hipLaunchKernelGGL((gemm_kernel<Tile<64, 128, 2, 2>, EPI_LOGMEL, false, false, false, false>),
+  hipLaunchKernelGGL((gemm_kernel<Tile<64, 64, 2, 2>, EPI_LOGMEL, false, false, false, false>),
                      dim3((m.M + 63) / 64), block, 0, st, m);
   return hipGetLastError();
 }
