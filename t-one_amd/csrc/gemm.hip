@@ -1111,11 +1111,22 @@ hipError_t mel_gemms(const float* wave, const float* basis_p, const float* fbank
   a.C = power;
   a.ldc = kMelPowCols;
   a.M = B * geo.melT;
-  a.N = 2 * kMelPowCols;
   a.K = kWin;
   const dim3 block(256);
-  hipLaunchKernelGGL((gemm_kernel<Tile<64, 128, 2, 2>, EPI_POWER, false, false, false, false>),
-                     dim3(((a.M + 63) / 64) * (a.N / 128)), block, 0, st, a);
+  if (a.M >= 16384) {
+    // large batch: bins 0..95 only (the 81 real bins in three 32-bin Re | Im blocks; the fourth block of the packed
+    // basis is all zero and its power columns keep the buffer's zero fill), 64 x 64 tiles, one Re | Im pair per wave:
+    // 103 -> 89 us at M = 122880; at M = 7680 the 128-thread tiles are slower (15.2 vs 11.8 us), so the 64 x 128 tiles
+    // over all four blocks stay there (profiles/r04_power_bins96_ab.jsonl, r04_power_bins96_*_step_breakdown.txt)
+    static_assert(kBins <= 96 && kMelPowCols >= 96, "three 32-bin blocks cover the spectrum");
+    a.N = 2 * 96;
+    hipLaunchKernelGGL((gemm_kernel<Tile<64, 64, 2, 1>, EPI_POWER, false, false, false, false>),
+                       dim3(((a.M + 63) / 64) * (a.N / 64)), dim3(128), 0, st, a);
+  } else {
+    a.N = 2 * kMelPowCols;
+    hipLaunchKernelGGL((gemm_kernel<Tile<64, 128, 2, 2>, EPI_POWER, false, false, false, false>),
+                       dim3(((a.M + 63) / 64) * (a.N / 128)), block, 0, st, a);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   GemmArgs m{};
