@@ -406,6 +406,90 @@ def workload_line(name, res, n_streams, steps, dtype, chunk=C.AUDIO_CHUNK_SAMPLE
             "dtype": dtype, **extra, "roofline": res["roofline"]}
 
 
+_ROOF_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "traffic_unit", "traffic_source",
+              "algo_bytes", "traffic_over_algo", "avg_us", "flop_per_launch", "step_tflops", "encoder_gemm_tflops",
+              "encoder_gemm_frac", "gemm_roofline_frac", "step_io_gbs", "pipe_peak", "pipe_frac")
+_RESID_KEYS = ("bound", "avg_us", "achieved", "hbm_frac", "frac", "traffic", "traffic_over_algo")
+
+
+def summary_roofline(roof: dict | None, alt: bool = False) -> dict | None:
+    """The roofline fields the printed line keeps (the per-family tables stay in the detail file)."""
+    if roof is None:
+        return None
+    keys = ("kernel", "achieved", "peak", "frac", "avg_us", "encoder_gemm_frac", "traffic_over_algo") if alt else _ROOF_KEYS
+    out = {k: roof[k] for k in keys if k in roof}
+    if roof.get("resid_family"):
+        out["resid_family"] = {k: roof["resid_family"][k] for k in _RESID_KEYS if k in roof["resid_family"]}
+    return out
+
+
+def summary_line(out: dict, detail: str | None) -> dict:
+    s = {k: v for k, v in out.items() if k not in ("roofline", "alt_workloads", "cpu_baseline")}
+    s["roofline"] = summary_roofline(out["roofline"])
+    cpu = out["cpu_baseline"]
+    s["cpu_baseline"] = None if cpu is None else {k: v for k, v in cpu.items() if k != "per_batch"} | {
+        "b1": cpu["per_batch"]["b1"]["value"] if "b1" in cpu.get("per_batch", {}) else None}
+    s["alt_workloads"] = [{"workload": a["workload"].split(":")[0], "value": a["value"], "ms_per_step": a["ms_per_step"],
+                           "dtype": a["dtype"], "n_gpus": a.get("n_gpus"), "batch_per_gpu": a.get("batch_per_gpu"),
+                           "global_batch": a.get("global_batch"), "scaling": a.get("scaling"),
+                           "roofline": summary_roofline(a["roofline"], alt=True)} for a in out["alt_workloads"]]
+    s["detail"] = detail
+    return s
+
+
+def rank_envs(n: int, port: int, base_env: dict | None = None) -> list[dict]:
+    """The environment of each of n rank processes, as torchrun would set it (one process per GPU, rendezvous on
+    127.0.0.1)."""
+    base = dict(os.environ if base_env is None else base_env)
+    return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)) for r in range(n)]
+
+
+def spawn_ranks(n: int, argv: list[str], timeout_s: float | None = None, script: str | None = None) -> int:
+    """``python bench.py --gpus N`` without torchrun: start the N rank processes as children of this one (which has
+    not touched the GPU) and wait for them.  Rank 0's stdout (the JSON line) is passed through; if any rank fails,
+    the others are terminated (they would block in a collective) and the first failing exit status is returned."""
+    import signal
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-u", script or os.path.abspath(__file__)] + argv
+    procs = [subprocess.Popen(cmd, env=e, cwd=ROOT, start_new_session=True,
+                              stdout=None if r == 0 else subprocess.DEVNULL)
+             for r, e in enumerate(rank_envs(n, port))]
+    t_end = None if timeout_s is None else time.monotonic() + timeout_s
+    status = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and status == 0:
+            status = bad[0]
+        if all(c is not None for c in codes):
+            break
+        if bad or (t_end is not None and time.monotonic() > t_end):
+            status = status or 124
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGTERM)
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+            break
+        time.sleep(0.2)
+    if status < 0:
+        status = 128 - status          # killed by a signal
+    if status:
+        print(f"bench.py: a rank failed (exit status {status})", file=sys.stderr)
+    return status
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -432,8 +516,15 @@ def main() -> None:
     ap.add_argument("--dist-always", action="store_true",
                     help="initialise the process group even at N = 1 (torchrun --nproc-per-node 1): the weight broadcast, "
                          "the per-step logprob all-gather and the max-over-ranks reduction then run through RCCL on one GPU")
+    ap.add_argument("--spawn-timeout", type=float, default=1500.0,
+                    help="--gpus N > 1 without torchrun: seconds before the spawned ranks are terminated")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="file for the full per-family roofline of every leg (the printed line carries a summary)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launched as plain `python bench.py --gpus N`: this process starts the N ranks itself (before any GPU call)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.spawn_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -535,7 +626,18 @@ def main() -> None:
             "latency_b1": lat,
             "alt_workloads": alts,
         }
-        print(json.dumps(out), flush=True)
+        # the full line (per-family rooflines of every leg) goes to a file; the printed line carries a summary
+        # short enough for a driver's stdout tail to hold all of it
+        detail = None
+        if args.detail:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+                with open(args.detail, "w") as fh:
+                    json.dump(out, fh, indent=1)
+                detail = os.path.relpath(os.path.abspath(args.detail), ROOT)
+            except OSError:
+                detail = None
+        print(json.dumps(summary_line(out, detail)), flush=True)
     if pg is not None:
         pg.barrier()   # rank 0 finishes its roofline pass before any rank tears the communicator down
         pg.destroy_process_group()

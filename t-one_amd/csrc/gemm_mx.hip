@@ -831,6 +831,10 @@ hipError_t gemm_mx(const MxArgs& a0, int epi, hipStream_t st) {
   // spills at two waves per SIMD
   if (a.K % 128 || a.K / 32 > kMxKB || a.M <= 0 || a.lda % 16 || a.ldas % 4 || (a.ldc % 8) || a.N % 128)
     return hipErrorInvalidValue;
+  // the fused MXFP8 operand (Q8) quantizes the bf16 shadow's registers and indexes the sum-of-squares slab by
+  // 32-column block: RESID with a shadow, every output, and whole rows of 384 only (as gemm.hip checks C8)
+  if (a.Q8 && (epi != EPI_RESID || !a.C2 || !a.Q8s || !a.ss8 || a.N != 32 * kSsSlots || a.ldc != a.N))
+    return hipErrorInvalidValue;
   switch (epi) {
     case EPI_SWIGLU: return (!a.C8 || !a.C8s) ? hipErrorInvalidValue : launch_mx<128, EPI_SWIGLU>(a, st);
     // 128 X rows per tile while there are few 256-row tiles (FFN down at M = 10240: 22.0 vs 31.7 us, M = 2560-5120:

@@ -208,14 +208,21 @@ __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
   if constexpr (DWT > 0) {
     __syncthreads();                                     // the GLU tile is in LDS
     const int nb = p.M / DT;
-    for (int pr = lane; pr < nb * 16; pr += 64) {
+    // uniform trip count over the waves (the barrier below): every wave handles the same (stream, channel) pairs
+    for (int base = 0; base < nb * 16; base += 64) {
+      const int pr = base + lane;
+      if (base > 0) {   // streams 4 and up (B > 4): their state now, read by every wave before any wave writes
+        if (pr < nb * 16) {
+          const __half* st = p.dw.s.in + p.dw.s.row_in(pr >> 4) + kOffConv + (int64_t)p.dw.layer * kD * kConvS +
+                             (c0 + (pr & 15)) * kConvS;
+#pragma unroll
+          for (int i = 0; i < kConvS; ++i) dwx[i] = __half2float(st[i]);
+        }
+        __syncthreads();   // the state rows may be written in place (slots_out == slots)
+      }
+      if (pr >= nb * 16) continue;
       const int b = pr >> 4, cl = pr & 15, ch = c0 + cl;
       const int64_t sec = kOffConv + (int64_t)p.dw.layer * kD * kConvS + ch * kConvS;
-      if (pr >= 64) {   // streams 4 and up (B > 4): their state now
-        const __half* st = p.dw.s.in + p.dw.s.row_in(b) + sec;
-#pragma unroll
-        for (int i = 0; i < kConvS; ++i) dwx[i] = __half2float(st[i]);
-      }
       float x[kConvS + DT];
 #pragma unroll
       for (int i = 0; i < kConvS; ++i) x[i] = dwx[i];

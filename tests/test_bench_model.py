@@ -83,3 +83,53 @@ def test_measured_traffic_not_below_algorithmic():
         for fam, v in fams.items():
             ratio = v["traffic_bytes_per_launch"] / bench.algo_bytes(fam, prec, int(b))
             assert ratio >= 1.0, (path, fam, ratio)
+
+
+def test_rank_envs_like_torchrun():
+    envs = bench.rank_envs(4, 29512, {"PATH": "/bin"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"] and all(e["WORLD_SIZE"] == "4" for e in envs)
+    assert all(e["LOCAL_RANK"] == e["RANK"] and e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29512"
+               and e["PATH"] == "/bin" for e in envs)
+
+
+def test_spawn_ranks_passes_rank0_and_propagates_failure(tmp_path, capfd):
+    """`bench.py --gpus N` without torchrun starts N children (no GPU here: a stand-in rank script); rank 0's
+    stdout passes through, a failing rank's status comes back and the blocked ranks are terminated."""
+    ok = tmp_path / "ok.py"
+    ok.write_text("import os\nprint('rank', os.environ['RANK'], 'of', os.environ['WORLD_SIZE'])\n")
+    assert bench.spawn_ranks(3, [], 60, script=str(ok)) == 0
+    out = capfd.readouterr().out
+    assert "rank 0 of 3" in out and "rank 1" not in out          # only rank 0's stdout is passed through
+    bad = tmp_path / "bad.py"
+    bad.write_text("import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(3)\ntime.sleep(120)\n")
+    t0 = __import__("time").monotonic()
+    assert bench.spawn_ranks(2, [], 60, script=str(bad)) == 3
+    assert __import__("time").monotonic() - t0 < 30                # rank 0 was terminated, not waited for
+    hang = tmp_path / "hang.py"
+    hang.write_text("import time\ntime.sleep(120)\n")
+    assert bench.spawn_ranks(2, [], 2, script=str(hang)) == 124
+
+
+def test_summary_line_fits_driver_tail():
+    """The printed line keeps every leg's value / ms_per_step / roofline fraction and stays well inside the
+    driver's ~8 KB stdout tail; the per-family tables go to the detail file."""
+    fams = {f: {"us_per_step": 1.0, "bound": "hbm", "floor_us": 1.0, "frac": 0.5, "gb_per_step": 0.1}
+            for f in bench.GEMM_FAMILIES}
+    roof = {k: 1.0 for k in bench._ROOF_KEYS} | {"kernel": "gemm_ffn_up", "unit": "TFLOP/s", "bound": "mfma",
+                                                  "traffic_source": "profiles/r05_traffic_fp32_b256.json",
+                                                  "gemm_families": fams, "families_us_per_step": {f: 1.0 for f in fams},
+                                                  "resid_family": {k: 1.0 for k in bench._RESID_KEYS} | {"kernels": "x" * 80}}
+    alt = {"workload": "BASELINE config 4: " + "y" * 200, "value": 1.0, "ms_per_step": 1.0, "dtype": "bf16", "n_gpus": 8,
+           "batch_per_gpu": 512, "global_batch": 4096, "scaling": "strong", "roofline": roof}
+    out = {"metric": bench.METRIC, "value": 1.0, "roofline": roof, "alt_workloads": [alt] * 4,
+           "cpu_baseline": {"value": 1.0, "unit": "real-time streams", "cores": 16, "kind": "port", "sample": "z" * 200,
+                            "per_batch": {"b1": {"value": 20.0}, "b256": {"value": 190.0}}},
+           "latency_b1": {"device_step_median_ms": 1.0, "what": "w" * 200}, "config": {"workload": "c" * 100}}
+    s = bench.summary_line(out, "gpurun_out/bench_detail.json")
+    txt = __import__("json").dumps(s)
+    assert len(txt) < 6000, len(txt)
+    assert s["roofline"]["frac"] == 1.0 and "gemm_families" not in s["roofline"]
+    assert [a["workload"] for a in s["alt_workloads"]] == ["BASELINE config 4"] * 4
+    assert all(a["roofline"]["encoder_gemm_frac"] == 1.0 and a["roofline"]["resid_family"]["hbm_frac"] == 1.0
+               for a in s["alt_workloads"])
+    assert s["cpu_baseline"]["cores"] == 16 and s["cpu_baseline"]["b1"] == 20.0 and s["detail"]

@@ -331,9 +331,10 @@ def test_bf16_pre_encode_stage(weights, oracle):
     assert rel < 2e-2, rel
 
 
-@pytest.mark.parametrize("prec,b,n", [("bf16", 2048, 10), ("bf16", 4096, 10), ("fp8", 4096, 10)])
+@pytest.mark.parametrize("prec,b,n", [("bf16", 512, 10), ("bf16", 2048, 10), ("bf16", 4096, 10), ("fp8", 4096, 10)])
 def test_large_batch_staggered_streams(weights, oracle, prec, b, n):
-    """The bench's own workloads with the oracle: BASELINE config 3 (bf16, B = 2048) and the
+    """The bench's own workloads with the oracle: config 4's per-GPU shard at N = 8 (bf16, B = 512),
+    BASELINE config 3 (bf16, B = 2048) and the
     N = 1 legs of configs 4 / 5 (bf16 / fp8 at B = 4096, the batch bench.py times), 10 stateful 300 ms chunks,
     stream s starting (zero state) at chunk s % 4; 64 sampled streams stepped independently by the oracle
     (its own fp32 state chain, not the device state) and compared every chunk.  These batches route FFN up
@@ -499,7 +500,8 @@ def test_ragged_batches(weights, oracle, prec, b):
                 # near-tie frames -- measured 0.9905 (fp32 residual stream) and 0.981 (fp16, this tree) at B = 1000,
                 # 0.9929 at B = 2048 for both, 1.0 on the second chunk (scripts/r04_ragged_probe.py,
                 # profiles/r04_ragged_probe.txt); every flip is below the 1.0 margin, which stays strict
-                agree = 0.995 if prec == "bf16" else 0.975
+                # fp8: at most 4 flips of the 210 frames (the measured 0.981), all below the strict 1.0 margin
+                agree = 0.995 if prec == "bf16" else 1.0 - 4.5 / lp_o[..., 0].size
                 assert_bf16_close(lp_g[pick], lp_o, f"{prec} B={b} chunk {c}", bounds, agree)
     finally:
         s.close()
@@ -625,6 +627,58 @@ def test_hip_vs_exported_fp16_graph(sess):
     d = np.concatenate([x.ravel() for x in ds])
     print(f"HIP fp32 vs exported fp16 graph: max {d.max():.3g}, mean {d.mean():.3g}")
     assert d.max() < 2.5e-2 and d.mean() < 5e-3, (d.max(), d.mean())
+
+
+# bf16 / fp8 modes against the exported fp16 graph (golden_fp16.npz): both keep the residual stream in fp16 as that
+# graph does.  Measured on the MI355X (profiles/r05_fp16_graph_lowprec.txt): bounds about 1.5x the measured max / mean.
+FP16_GRAPH_BOUNDS = {"bf16": (0.1, 0.02), "fp8": (0.6, 0.1)}
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp8"])
+def test_lowprec_vs_exported_fp16_graph(weights, prec):
+    """The bf16 / fp8 modes (fp16 residual stream, as the exported graph keeps it, tone/scripts/export.py:411) against
+    the EXPORTED graph's numerics on the golden streams and the reference's example utterance, chunk by chunk: max and
+    mean |dlogp| within the mode's bound, greedy argmax identical wherever the graph's top-2 margin exceeds the mode's
+    argmax margin (BF16_MARGIN / FP8_MARGIN)."""
+    _gpu()
+    from tone_amd.model import ToneSession
+    g, gs = np.load(GOLDEN / "golden_fp16.npz"), np.load(GOLDEN / "golden_stream.npz")
+    margin = BF16_MARGIN if prec == "bf16" else FP8_MARGIN
+    s = ToneSession(weights, precision=prec, max_batch=4)
+    ds, flips, frames = [], 0, 0
+
+    def check(lp, ref, what):
+        nonlocal flips, frames
+        ds.append(np.abs(lp - ref).ravel())
+        srt = np.sort(ref, axis=-1)
+        clear = (srt[..., -1] - srt[..., -2]) > margin
+        np.testing.assert_array_equal(lp.argmax(-1)[clear], ref.argmax(-1)[clear], err_msg=what)
+        flips += int((lp.argmax(-1) != ref.argmax(-1)).sum())
+        frames += lp[..., 0].size
+
+    try:
+        pcm = gs["pcm"].astype(np.int32)
+        B, N = pcm.shape[:2]
+        st = np.zeros((B, C.STATE_SIZE), np.float16)
+        for c in range(N):
+            st[np.arange(B) > c] = 0
+            lp, st = gpu_step(s, pcm[:, c], st)
+            check(lp, g["stream_logprobs"][:, c], f"{prec} stream chunk {c}")
+        audio = np.load(GOLDEN / "audio_short_pcm.npy").astype(np.int32)
+        padded = np.pad(audio, (2400, 2400))
+        padded = np.pad(padded, (0, -len(padded) % 2400)).reshape(-1, 2400)
+        st1 = np.zeros((1, C.STATE_SIZE), np.float16)
+        for i, ch in enumerate(padded):
+            lp, st1 = gpu_step(s, ch[None], st1)
+            check(lp[0], g["audio_logprobs"][i], f"{prec} audio chunk {i}")
+    finally:
+        s.close()
+    d = np.concatenate(ds)
+    print(f"HIP {prec} vs exported fp16 graph: max {d.max():.3g}, mean {d.mean():.3g}, p99 {np.percentile(d, 99):.3g}, "
+          f"argmax flips {flips}/{frames}")
+    mx, mean = FP16_GRAPH_BOUNDS[prec]
+    assert d.max() < mx and d.mean() < mean, (d.max(), d.mean())
+    assert flips <= 0.005 * frames, (flips, frames)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp8"])

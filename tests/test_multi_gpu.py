@@ -74,3 +74,24 @@ def test_bench_rccl_world1():
     assert out["config"]["collective"] and "RCCL" in out["config"]["collective"]
     c4, c5 = out["alt_workloads"]
     assert c4["value"] > 0 and c5["value"] > 0 and c5["dtype"] == "fp8"
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_without_torchrun(tmp_path):
+    """The driver's launch form: plain `python bench.py --gpus 2` (no torchrun, WORLD_SIZE unset) starts its two
+    rank processes itself (gloo here: the box has one card) and prints one line with n_gpus 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "4"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--steps", "4",
+                        "--warmup", "1", "--batch", "16", "--alt", "0", "--config4", "64", "--config5", "0",
+                        "--cpu-baseline-s", "0", "--detail", str(tmp_path / "detail.json")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["config"]["global_batch"] == 32 and out["value"] > 0
+    (c4,) = out["alt_workloads"]
+    assert c4["n_gpus"] == 2 and c4["batch_per_gpu"] == 32 and c4["value"] > 0
+    full = json.loads((tmp_path / "detail.json").read_text())
+    assert "gemm_families" in full["roofline"] and full["value"] == out["value"]
