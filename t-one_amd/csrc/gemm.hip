@@ -895,6 +895,11 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st, bool* c8
   constexpr int kTarget = 512;
   *c8_done = false;
   // large batches: the persistent transposed-orientation kernels (gemm_t.hip, tools/gemm_bench sweep)
+  // the residual-output projections (N = 384) at large M: whole rows per workgroup (gemm_rp.hip)
+  if (epi == EPI_RESID && a.res16 && a.N == 384 && gemm_rp_routed(a.M, a.K)) {
+    *c8_done = true;
+    return gemm_rp(a, st);
+  }
   const int64_t t256 = (int64_t)((a.M + 255) / 256) * (a.N / 256);
   // K = 384 paired projections from 40 (SwiGLU) / 60 (GLU) blocks of 256 rows up: the X-stationary kernel
   // (round 3's gemm_xs: FFN up M = 40960: 114 vs 165 us for gemm_t, M = 10240: 37 vs 41; pw1 M = 40960: 42 vs 47,
@@ -991,6 +996,10 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   // the depthwise conv in the GLU epilogue exists on gemm_sm only (fp32 mode, M <= 64): no other route
   if (a.dw.w) return (!bf16 && epi == EPI_GLU && a.M <= 64) ? gemm_sm(a, epi, st) : hipErrorInvalidValue;
   if (a.att.probs) return (!bf16 && epi == EPI_RESID && a.M <= 64) ? gemm_sm(a, epi, st) : hipErrorInvalidValue;
+  // a fused row norm exists on the row-panel kernel only
+  if (a.norm_w)
+    return (bf16 && a.a_bf16 && epi == EPI_RESID && a.res16 && gemm_rp_routed(a.M, a.K)) ? gemm_rp(a, st)
+                                                                                       : hipErrorInvalidValue;
   // the fp16 residual stream exists in the bf16 / fp8 modes only (the LDS-DMA and f32t kernels of gemm_bf16)
   if (a.res16 && (!bf16 || !a.a_bf16 || a.c_bf16 || (epi != EPI_STORE && epi != EPI_RESID))) return hipErrorInvalidValue;
   if (bf16 && a.a_bf16) {

@@ -77,9 +77,16 @@ struct GemmArgs {
                       // writes C as fp16 (the shadow C2 stays bf16)
   DwFuse dw;          // EPI_GLU on gemm_sm only: the depthwise conv in the epilogue (C is not written)
   AttFuse att;        // EPI_RESID, K = 384 on gemm_sm only: A = ctx computed from P and V (A is not read)
+  const float* norm_w; // EPI_RESID on the row-panel kernel only (gemm_rp): RMSNorm (gain norm_w) of each whole output
+                       // row after the residual add; C and its shadows hold the normalized row
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
+// Row-panel residual GEMM (gemm_rp.hip): bf16 A / W, N = 384, the fp16 residual stream updated in place with the whole
+// output row per workgroup (optional fused RMSNorm, norm_w); bm = panel rows (0: about one panel per CU)
+hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm = 0);
+// whether gemm() routes a bf16-mode RESID projection of M rows and depth K to gemm_rp (so a norm can be fused)
+bool gemm_rp_routed(int M, int K);
 
 // W tiles per work item of the X-stationary MXFP8 kernel (gemm_xs8: one 256-row X block, one workgroup per
 // CU): the run length minimising rounds x (run + 3), 3 tiles being the per-item cost of loading the X fragments and

@@ -391,8 +391,10 @@ struct Scope {
 int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, int64_t lda, const void* W, void* C,
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
               float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr,
-              bool mx_out = false, const DwFuse* dw = nullptr, const AttFuse* att = nullptr) {
+              bool mx_out = false, const DwFuse* dw = nullptr, const AttFuse* att = nullptr,
+              const float* norm_w = nullptr) {
   GemmArgs a{};   // value-initialised: every field not set below is zero
+  a.norm_w = norm_w;
   if (dw) a.dw = *dw;
   if (att) a.att = *att;
   a.A = A;
@@ -529,6 +531,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     const LayerW& w = s->L[l];
     const int M = B * T;
     const void* xa = bf ? static_cast<const void*>(xs) : x;   // A operand of the rowscale GEMMs
+    // bf16 mode: norm_out runs inside FFN2's down-projection when that launch is a row-panel one (whole rows)
+    const bool norm_fused = bf && !f8 && gemm_rp_routed(M, kDff);
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
     // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
     // up-projection's epilogue
@@ -546,8 +550,9 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       }
       CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[f], s->h, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
                      1.0f, true, true));
+      // FFN2's down-projection on the row-panel kernel also applies the block-final RMSNorm (norm_out)
       return gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
-                       false, xs);
+                       false, xs, false, nullptr, nullptr, f == 1 && norm_fused ? w.norm_out : nullptr);
     };
     CALL(ffn(0));
     // MHSA (conformer_blocks.py:816-825)
@@ -644,7 +649,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     CALL(ffn(1));
     // the next layer's FFN1 reads this norm's output unless the reduction / upsampling comes in between
     q8_fresh = f8n && l != 6 && l < 14;
-    LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, bf, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->ss8));
+    if (!norm_fused)
+      LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, bf, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->ss8));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
       LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, geo.T, st));
       CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * geo.Tr, D, 4 * D,

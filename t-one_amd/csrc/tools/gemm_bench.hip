@@ -199,6 +199,8 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   fflush(stdout);
 }
 
+static const int kRpRows[9] = {0, 16, 32, 48, 64, 80, 96, 128, 160};
+
 int main(int argc, char** argv) {
   if (argc < 6) { fprintf(stderr, "usage: %s M K N epi v1,v2,.. [nsplit] [iters]\n", argv[0]); return 2; }
   const int M = atoi(argv[1]), K = atoi(argv[2]), N = atoi(argv[3]), epi = atoi(argv[4]);
@@ -320,6 +322,7 @@ int main(int argc, char** argv) {
     auto launch = [&]() {
       return vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
+             : (v >= 90 && v <= 98) ? gemm_rp(a, 0, kRpRows[v - 90])   // 90: auto panel rows, 91-98: 16 .. 160
              : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
              : v >= 60 ? gemm_x3(a, epi, v - 60, 0)
              : (v >= 50 && nsplit > 1) ? gemm_x3_splitk(a, epi, v - 50, nsplit, 0)
