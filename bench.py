@@ -501,6 +501,8 @@ def main() -> None:
                          "replaces --batch for the headline")
     ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "bf16", "fp8"], default="fp32")
     ap.add_argument("--chunks", type=int, default=10, help="distinct 300 ms chunks cycled per stream")
+    ap.add_argument("--chunk-samples", type=int, default=C.AUDIO_CHUNK_SAMPLES, choices=[2400, 3200],
+                    help="headline leg's chunk: 2400 (300 ms, BASELINE) or 3200 (the 400 ms variant; A/B runs)")
     ap.add_argument("--cpu-baseline-s", type=float, default=8.0, help="CPU baseline budget per batch (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -549,10 +551,10 @@ def main() -> None:
         B, cap, total, scaling = sizes[rank], max(sizes), args.global_batch, "strong"
     else:
         B, cap, total, scaling = args.batch, args.batch, world * args.batch, "weak"
-    res = measure(args, B, args.precision, dev, local, world, rank, pg, cap=cap)
+    res = measure(args, B, args.precision, dev, local, world, rank, pg, cap=cap, chunk=args.chunk_samples)
     ms_step = res["elapsed"] / args.steps * 1e3
     chunks_s = total / (res["elapsed"] / args.steps)
-    streams = chunks_s * C.AUDIO_CHUNK_SAMPLES / C.SAMPLE_RATE
+    streams = chunks_s * args.chunk_samples / C.SAMPLE_RATE
 
     alts = []
     # BASELINE config 3 (1 GPU, batch 2048, bf16 MFMA, stateful) reported beside the headline

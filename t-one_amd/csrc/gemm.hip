@@ -1039,16 +1039,24 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
         return gemm_x3(a, epi, 9, st);
       }
     }
-    if (epi == EPI_SWIGLU && a.N % 256 == 0)
-      return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 256) >= 200 ? 7 : 6, st);
+    // FFN up: 128 W x 256 X tiles while they fill the CUs at most once (M = 1536 / 2560: 38.1 / 45.2 vs 45.5 / 47.8 us
+    // for the previous 256 x 128 / 128 x 128 routes), 128 x 128 tiles otherwise (M = 3328, the 400 ms full layers: 70.5
+    // vs 82.4; M = 1280: 25.5) (scripts/r05_x3_sweep2.sh, profiles/r05_x3_sweep2.jsonl, three interleaved runs)
+    if (epi == EPI_SWIGLU && a.N % 256 == 0) {
+      const int64_t t8 = (int64_t)((a.M + 255) / 256) * (a.N / 128);
+      return gemm_x3(a, epi, (t8 > 128 && t8 <= 256) ? 8 : 6, st);
+    }
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
     if (epi == EPI_GLU && a.N % 128 == 0) return gemm_x3(a, epi, 1, st);
-    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N >= 1024 && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
+    // q|k|v (N = 1152): 128 W x 64 X tiles below ~128 tiles of 128 x 128 (M = 1280 / 1536: 15.5 / 16.3 vs 22.7 / 23.1 us)
+    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N >= 1024 && a.N % 128 == 0)
+      return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 128) < 128 ? 1 : 6, st);
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0 && a.K % 128 == 0 &&
-        (int64_t)((a.M + 63) / 64) * (a.N / 64) <= 160)
-      // few 64x64 tiles (the reduced layers at B = 256, M = 1280): 32x64 tiles with a four-way in-WG
+        (int64_t)((a.M + 63) / 64) * (a.N / 32) <= 256)
+      // up to one 32x64 tile per CU (the reduced layers at B = 256, M = 1280): 32x64 tiles with a four-way in-WG
       // K split fill twice the CUs; beats split-K on FFN down (19.1 vs 22.2 us) and the 64x64 tile on the
-      // K = 384 projections (8.1 vs 11.1 us) (scripts/x3n_sweep.sh, profiles/r01_x3n_sweep_b256.jsonl)
+      // K = 384 projections (8.1 vs 11.1 us) (scripts/x3n_sweep.sh, profiles/r01_x3n_sweep_b256.jsonl); past one per
+      // CU the 64x64 tile (M = 1536, the 400 ms reduced layers: FFN down 28.4 vs 34.3 us, K = 384 10.9 vs 13.8)
       return gemm_x3(a, epi, 10, st);
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_x3(a, epi, 0, st);
   }

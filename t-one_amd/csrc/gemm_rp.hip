@@ -344,8 +344,10 @@ static int gemm_rp_panel_rows(int M) {
 }
 
 bool gemm_rp_routed(int M, int K) {
-  // from about one 48-row panel per CU (tools/gemm_bench variants 90-98)
-  return K % 32 == 0 && M >= 10240;
+  // from 64-row panels (M >= 16384): at M = 20480 (80-row panels) 40 vs 45 us (K = 1536) and 18 vs 21 (K = 384) for
+  // the LDS-DMA 128 x 128 tiles, at M = 10240 (48 rows) 31 vs 24 and 13.5 vs 11.2 (tools/gemm_bench variants 14 / 90,
+  // profiles/r05_rp_sweep_readahead.jsonl): the W fill per CU no longer shrinks with the panel
+  return K % 32 == 0 && M >= 16384;
 }
 
 hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm) {

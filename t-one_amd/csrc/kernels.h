@@ -13,6 +13,7 @@ namespace tone {
 // processes).  Defaults are the measured best; none of them changes the arithmetic.
 struct Knobs {
   int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand
+  int rp_norm;         // TONE_RP_NORM=0: norm_out as its own launch instead of inside FFN2 down (gemm_rp)
 };
 const Knobs& knobs();
 

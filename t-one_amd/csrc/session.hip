@@ -32,6 +32,7 @@ const Knobs& knobs() {
     };
     Knobs r;
     r.fp8_normq = env("TONE_FP8_NORMQ", 1) != 0;
+    r.rp_norm = env("TONE_RP_NORM", 1) != 0;
     return r;
   }();
   return k;
@@ -532,7 +533,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     const int M = B * T;
     const void* xa = bf ? static_cast<const void*>(xs) : x;   // A operand of the rowscale GEMMs
     // bf16 mode: norm_out runs inside FFN2's down-projection when that launch is a row-panel one (whole rows)
-    const bool norm_fused = bf && !f8 && gemm_rp_routed(M, kDff);
+    const bool norm_fused = bf && !f8 && knobs().rp_norm && gemm_rp_routed(M, kDff);
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
     // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
     // up-projection's epilogue

@@ -290,6 +290,15 @@ int main(int argc, char** argv) {
   }
   a.rowscale = rowscale;
   a.inv_sqrt_k = 1.0f / sqrtf((float)K);
+  // NORMW=1: RESID with the fused row RMSNorm (gemm_rp only; gain = 1 + small noise). The error check then compares
+  // against the un-normalized reference (timing only)
+  float* normw = nullptr;
+  if (getenv("NORMW") && atoi(getenv("NORMW"))) {
+    std::vector<float> g(N);
+    for (auto& v : g) v = 1.0f + 0.1f * rnd();
+    CK(hipMalloc(&normw, N * 4));
+    CK(hipMemcpy(normw, g.data(), N * 4, hipMemcpyHostToDevice));
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const double flop = 2.0 * M * N * (double)K;
@@ -319,6 +328,7 @@ int main(int argc, char** argv) {
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
     a.res16 = res16 && !f32;
+    a.norm_w = (v >= 90 && v <= 98) ? normw : nullptr;
     auto launch = [&]() {
       return vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
