@@ -46,9 +46,16 @@ struct RpCfg {
   static constexpr int kStage = (BM + kRpN) * kRpRowB;
   static constexpr int kImg = (2 * 16 * kRpPitch + 2 * kRpN) * 4;   // the epilogue's two 16-row image slots + bias / gain
   static constexpr int kLds = kRpS * kStage > kImg ? kRpS * kStage : kImg;
+  // MXFP8 (fp8 mode): a stage is one 128-deep K-tile: A rows | W rows (128 B each) | the K-tile's 4 scale bytes per
+  // A row (whole 256-byte DMA pieces) | per W row; two stages
+  static constexpr int kMxScA = (BM + kRpN) * 128, kMxScW = kMxScA + (BM + 63) / 64 * 256;
+  static constexpr int kMxStage = kMxScW + kRpN * 4;
+  static constexpr int QA = BM / 8, QW = kRpN / 8, QAS = (BM + 63) / 64, QWS = kRpN / 64;   // DMA pieces per stage
+  static constexpr int QN = QA + QW + QAS + QWS, QP = (QN + 7) / 8;
+  static constexpr int kLdsMx = 2 * kMxStage > kImg ? 2 * kMxStage : kImg;
   static constexpr int NV = 3;                             // 16-byte vectors per lane per row (32 lanes x 3 x 4 = 384)
   static_assert(WM * WN == 8 && FN * WN == 24, "8 waves over the panel");
-  static_assert(kLds <= 160 * 1024, "LDS");
+  static_assert(kLds <= 160 * 1024 && kLdsMx <= 160 * 1024, "LDS");
 };
 
 template <int N>
@@ -83,20 +90,48 @@ __device__ __forceinline__ float rp_max8(float v) {    // over each 8-lane group
   return fmaxf(v, rp_dpp<0x141>(v));
 }
 
-// NORM: RMSNorm the output row (gain p.norm_w); Q8: fp8 mode, also the MXFP8 form of the shadow + the slab
-template <int WM, int FM, bool NORM, bool Q8>
-__global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(GemmArgs p) {
+typedef int rp_i32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int rp_u32x4 __attribute__((ext_vector_type(4)));
+
+// the kernel's arguments, from a GemmArgs (bf16 operands) or an MxArgs (MXFP8 operands)
+struct RpArgs {
+  const void* A;         // bf16 [M][K] (lda elements) or e4m3 [M][K] (lda bytes)
+  int64_t lda;
+  const uint8_t* As;     // MX: E8M0 [M][K/32] (ldas bytes)
+  int64_t ldas;
+  const void* W;         // bf16 or e4m3 [384][K]
+  const uint8_t* Ws;     // MX: E8M0 [384][K/32]
+  const float* bias;     // [384] or nullptr
+  const void* R;         // fp16 residual (ldr elements); C may alias it
+  int64_t ldr;
+  void* C;               // fp16 [M][384] (ldc elements)
+  int64_t ldc;
+  uint16_t* C2;          // bf16 shadow or nullptr
+  uint8_t* C8;           // Q8: the shadow's MXFP8 form [M][ldc], E8M0 [M][ldc / 32], sum-of-squares slab
+  uint8_t* C8s;
+  float* ss8;
+  const float* norm_w;   // NORM: the row RMSNorm's gain
+  float alpha;
+  int M, K, dbg;
+};
+
+// NORM: RMSNorm the output row (gain p.norm_w); Q8: fp8 mode, also the MXFP8 form of the shadow + the slab;
+// MX: MXFP8 operands (v_mfma_scale_f32_16x16x128_f8f6f4), else bf16 (v_mfma_f32_16x16x32_bf16)
+template <int WM, int FM, bool NORM, bool Q8, bool MX>
+__global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
   using Cfg = RpCfg<WM, FM>;
   constexpr int BM = Cfg::BM, RP = Cfg::RP, FN = Cfg::FN, NA = Cfg::NA, NV = Cfg::NV;
   constexpr int PMAX = Cfg::PMAX;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[Cfg::kLds];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[MX ? Cfg::kLdsMx : Cfg::kLds];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / Cfg::WN, wn = wid % Cfg::WN;
-  const int nk = p.K / 32;
+  const int nk = p.K / (MX ? 128 : 32);
   const int npan = (p.M + BM - 1) / BM;
   const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
   const uint16_t* __restrict__ W = static_cast<const uint16_t*>(p.W);
+  [[maybe_unused]] const uint8_t* __restrict__ A8 = static_cast<const uint8_t*>(p.A);
+  [[maybe_unused]] const uint8_t* __restrict__ W8 = static_cast<const uint8_t*>(p.W);
   const int np = wid < Cfg::NHI ? Cfg::PMAX : Cfg::PMIN;   // this wave's DMA pieces per stage (wave-uniform)
 #ifdef RP_ABLATE
   // microbenchmark ablations (tools/gemm_bench, gemm_bench_ablate; timing only, results wrong): 1 no epilogue, 4 no K
@@ -168,58 +203,157 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(GemmArgs p) {
                                                       4 * (eq + 32 * i));
     };
 
-    // fragments of a stage (the lane's swizzled 16-byte chunk of each 16-row block)
-    auto read_frags = [&](int slot, bf16x8(&fa)[FM], bf16x8(&fb)[FN]) {
-      const uint8_t* st = lds + slot * Cfg::kStage;
+    if constexpr (MX) {
+      // MXFP8: two stages of one 128-deep K-tile; stage kt + 1 is DMA'd while stage kt's MFMAs run.  The pieces of a
+      // stage (8 rows x 128 B for A / W, 64 rows x 4 scale bytes for As / Ws) are dealt over the waves, piece q to wave
+      // q % 8; a 128-byte row's chunk c sits at slot c ^ ((r >> 1) & 7) (gemm_mx.hip's swizzle: both fragment reads
+      // conflict-free)
+      constexpr int QA = Cfg::QA, QW = Cfg::QW, QAS = Cfg::QAS, QP = Cfg::QP;
+      const int nq = (Cfg::QN - wid + 7) / 8;   // this wave's pieces (wave-uniform)
+      // addresses are recomputed where they are used from an opaque copy of the lane id: hoisted out of the loop they
+      // were ~30 loop-invariant VGPRs (and spills)
+      auto stage_mx = [&](int slot, int kt) {
+        if (dbg & 8) return;
+        uint8_t* base = lds + slot * Cfg::kMxStage;
+        (void)base;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8*>(st + (wm * RP + 16 * i) * kRpRowB + frag_off);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(st + (BM + (wn * FN + j) * 16) * kRpRowB + frag_off);
-    };
-    auto wait_stage = [&](int younger) {   // this wave's DMAs of a stage landed, `younger` later stages may fly
-      if (np == Cfg::PMAX) rp_wait<Cfg::PMAX>(younger);
-      else rp_wait<Cfg::PMIN>(younger);
-    };
-    // read-ahead ring: stage kt + 1's fragments are read while stage kt's MFMAs run (from registers), so no MFMA
-    // waits on LDS; stage kt's slot is refilled with stage kt + S right after the barrier that follows its reads
-    const int nkl = (dbg & 4) ? 0 : nk;
-#pragma unroll
-    for (int s0 = 0; s0 < kRpS; ++s0)
-      if (s0 < nkl) stage(s0, s0);
-    // two fragment sets, alternating (the loop is unrolled by two so no set is copied)
-    bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
-    wait_stage(max(0, min(kRpS - 1, nkl - 1)));
-    barrier_lds();
-    read_frags(0, a0, b0);   // unconditional, as in the loop
-    auto step = [&](int kt, bf16x8(&a)[FM], bf16x8(&b)[FN], bf16x8(&na)[FM], bf16x8(&nb)[FN]) {
-      if (kt + 1 < nkl) wait_stage(min(kRpS - 2, nkl - 2 - kt));
-      barrier_lds();   // stage kt + 1 published; every wave's reads of stage kt are done, its slot is free
-      if (kt + kRpS < nkl) stage(kt % kRpS, kt + kRpS);
-      if (kt == nkl - 1) {
-#pragma unroll
-        for (int s = 0; s < kPreLoop; ++s) load_res(s);
-      }
-      read_frags((kt + 1) % kRpS, na, nb);   // unconditional (the last step reads a spent slot): a conditional read
-                                             // made the compiler merge and split the fragment vectors per element
-#ifdef RP_ABLATE
-      if (dbg & 16) {   // (element reads of the fragments in any build split them into 16-bit halves: ablation only)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j][0] += (float)a[i][0] * (float)b[j][0];
-        return;
-      }
+        for (int j = 0; j < QP; ++j) {
+          if (j >= nq) break;
+          [[maybe_unused]] const int q = wid + 8 * j;
+          if (q < QA + QW) {
+            const int r = 8 * (q < QA ? q : q - QA) + (ln >> 3), c = (ln & 7) ^ ((r >> 1) & 7);
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (q < QA)
+              __builtin_amdgcn_global_load_lds(A8 + (uint32_t)(min(m0 + r, p.M - 1) * p.lda + 128 * kt + 16 * c),
+                                               base + q * 1024, 16, 0, 0);
+            else
+              __builtin_amdgcn_global_load_lds(W8 + (uint32_t)(r * p.K + 128 * kt + 16 * c), base + BM * 128 + (q - QA) * 1024,
+                                               16, 0, 0);
+#else
+            (void)c;
 #endif
+          } else {
+            const int r = 64 * (q < QA + QW + QAS ? q - QA - QW : q - QA - QW - QAS) + ln;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (q < QA + QW + QAS)
+              __builtin_amdgcn_global_load_lds(p.As + (uint32_t)(min(m0 + r, p.M - 1) * p.ldas + 4 * kt),
+                                               base + Cfg::kMxScA + (q - QA - QW) * 256, 4, 0, 0);
+            else
+              __builtin_amdgcn_global_load_lds(p.Ws + (uint32_t)(r * (p.K / 32) + 4 * kt),
+                                               base + Cfg::kMxScW + (q - QA - QW - QAS) * 256, 4, 0, 0);
+#else
+            (void)r;
+#endif
+          }
+        }
+      };
+      const int nkl = (dbg & 4) ? 0 : nk;
+      if (nkl > 0) stage_mx(0, 0);
+      for (int kt = 0; kt < nkl; ++kt) {
+        rp_vmcnt<0>();   // stage kt landed (the only one in flight)
+        barrier_lds();   // ... for every wave; every wave's reads of stage kt - 1 are done, its slot is free
+        if (kt + 1 < nkl) stage_mx((kt + 1) & 1, kt + 1);
+        if (kt == nkl - 1) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+          for (int s = 0; s < kPreLoop; ++s) load_res(s);
+        }
+        // fragment bases: the lane's row l & 15 of the wave's first 16-row block, chunks (l >> 4) and 4 + (l >> 4) at
+        // their swizzled slots, scale byte (l >> 4) of the row; the other blocks are immediate offsets (2 KiB / 64 B)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int l15 = ln & 15, lg = ln >> 4, g = (l15 >> 1) & 7;
+        const uint8_t* st = lds + (kt & 1) * Cfg::kMxStage;
+        const uint8_t* pa = st + (wm * RP + l15) * 128;
+        const uint8_t* pw = st + (BM + wn * FN * 16 + l15) * 128;
+        const uint8_t* psa = st + Cfg::kMxScA + 4 * (wm * RP + l15) + lg;
+        const uint8_t* psw = st + Cfg::kMxScW + 4 * (wn * FN * 16 + l15) + lg;
+        const int c0 = 16 * (lg ^ g), c1 = 16 * ((4 + lg) ^ g);
+        auto frag = [&](const uint8_t* row) {
+          const rp_u32x4 a = *reinterpret_cast<const rp_u32x4*>(row + c0);
+          const rp_u32x4 b = *reinterpret_cast<const rp_u32x4*>(row + c1);
+          return rp_i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+        };
+        rp_i32x8 af[FM];
+        int as[FM];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    };
-    for (int kt = 0; kt < nkl; kt += 2) {
-      step(kt, a0, b0, a1, b1);
-      if (kt + 1 < nkl) step(kt + 1, a1, b1, a0, b0);
+        for (int i = 0; i < FM; ++i) {
+          af[i] = frag(pa + 2048 * i);
+          as[i] = psa[64 * i];
+        }
+        // W fragments one column tile ahead of its MFMAs (two register sets: all six at once spilled)
+        rp_i32x8 wf[2];
+        int ws[2];
+        auto rdw = [&](int j, int b) {
+          wf[b] = frag(pw + 2048 * j);
+          ws[b] = psw[64 * j];
+        };
+        rdw(0, 0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if (j + 1 < FN) rdw(j + 1, (j + 1) & 1);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], wf[j & 1], acc[i][j], 0, 0, 0, as[i], 0,
+                                                                         ws[j & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+      // fragments of a stage (the lane's swizzled 16-byte chunk of each 16-row block)
+      auto read_frags = [&](int slot, bf16x8(&fa)[FM], bf16x8(&fb)[FN]) {
+        const uint8_t* st = lds + slot * Cfg::kStage;
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8*>(st + (wm * RP + 16 * i) * kRpRowB + frag_off);
+  #pragma unroll
+        for (int j = 0; j < FN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8*>(st + (BM + (wn * FN + j) * 16) * kRpRowB + frag_off);
+      };
+      auto wait_stage = [&](int younger) {   // this wave's DMAs of a stage landed, `younger` later stages may fly
+        if (np == Cfg::PMAX) rp_wait<Cfg::PMAX>(younger);
+        else rp_wait<Cfg::PMIN>(younger);
+      };
+      // read-ahead ring: stage kt + 1's fragments are read while stage kt's MFMAs run (from registers), so no MFMA
+      // waits on LDS; stage kt's slot is refilled with stage kt + S right after the barrier that follows its reads
+      const int nkl = (dbg & 4) ? 0 : nk;
+  #pragma unroll
+      for (int s0 = 0; s0 < kRpS; ++s0)
+        if (s0 < nkl) stage(s0, s0);
+      // two fragment sets, alternating (the loop is unrolled by two so no set is copied)
+      bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+      wait_stage(max(0, min(kRpS - 1, nkl - 1)));
+      barrier_lds();
+      read_frags(0, a0, b0);   // unconditional, as in the loop
+      auto step = [&](int kt, bf16x8(&a)[FM], bf16x8(&b)[FN], bf16x8(&na)[FM], bf16x8(&nb)[FN]) {
+        if (kt + 1 < nkl) wait_stage(min(kRpS - 2, nkl - 2 - kt));
+        barrier_lds();   // stage kt + 1 published; every wave's reads of stage kt are done, its slot is free
+        if (kt + kRpS < nkl) stage(kt % kRpS, kt + kRpS);
+        if (kt == nkl - 1) {
+  #pragma unroll
+          for (int s = 0; s < kPreLoop; ++s) load_res(s);
+        }
+        read_frags((kt + 1) % kRpS, na, nb);   // unconditional (the last step reads a spent slot): a conditional read
+                                               // made the compiler merge and split the fragment vectors per element
+  #ifdef RP_ABLATE
+        if (dbg & 16) {   // (element reads of the fragments in any build split them into 16-bit halves: ablation only)
+  #pragma unroll
+          for (int i = 0; i < FM; ++i)
+  #pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j][0] += (float)a[i][0] * (float)b[j][0];
+          return;
+        }
+  #endif
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+  #pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      };
+      for (int kt = 0; kt < nkl; kt += 2) {
+        step(kt, a0, b0, a1, b1);
+        if (kt + 1 < nkl) step(kt + 1, a1, b1, a0, b0);
+      }
     }
     if (dbg & 4) {
 #pragma unroll
@@ -316,25 +450,23 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(GemmArgs p) {
   }
 }
 
-template <int WM, int FM>
-hipError_t launch_rp(const GemmArgs& a, hipStream_t st) {
+template <int WM, int FM, bool MX>
+hipError_t launch_rp(const RpArgs& a, hipStream_t st) {
   using Cfg = RpCfg<WM, FM>;
   const int npan = (a.M + Cfg::BM - 1) / Cfg::BM;
   const dim3 grid(npan < 256 ? npan : 256), block(kRpThreads);
   const bool q8 = a.C8 != nullptr;
   if (a.norm_w) {
-    if (q8) hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, true, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, true, false>), grid, block, 0, st, a);
+    if (q8) hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, true, true, MX>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, true, false, MX>), grid, block, 0, st, a);
   } else {
-    if (q8) hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, false, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, false, false>), grid, block, 0, st, a);
+    if (q8) hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, false, true, MX>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, false, false, MX>), grid, block, 0, st, a);
   }
   return hipGetLastError();
 }
 
-}  // namespace
-
-static int gemm_rp_panel_rows(int M) {
+int gemm_rp_panel_rows(int M) {
   // the smallest panel that keeps the panels within one per CU (256), from the instantiated heights
   const int need = (M + 255) / 256;
   const int rows[] = {16, 32, 48, 64, 80, 96, 128, 160};
@@ -342,6 +474,23 @@ static int gemm_rp_panel_rows(int M) {
     if (r >= need) return r;
   return 160;
 }
+
+template <bool MX>
+hipError_t launch_rp_bm(const RpArgs& a, int bm, hipStream_t st) {
+  switch (bm > 0 ? bm : gemm_rp_panel_rows(a.M)) {
+    case 16: return launch_rp<1, 1, MX>(a, st);
+    case 32: return launch_rp<1, 2, MX>(a, st);
+    case 48: return launch_rp<1, 3, MX>(a, st);
+    case 64: return launch_rp<1, 4, MX>(a, st);
+    case 80: return launch_rp<1, 5, MX>(a, st);
+    case 96: return launch_rp<2, 3, MX>(a, st);
+    case 128: return launch_rp<2, 4, MX>(a, st);
+    case 160: return launch_rp<2, 5, MX>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
 
 bool gemm_rp_routed(int M, int K) {
   // from 64-row panels (M >= 16384): at M = 20480 (80-row panels) 40 vs 45 us (K = 1536) and 18 vs 21 (K = 384) for
@@ -355,17 +504,24 @@ hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm) {
       a.ldc % 8 || a.ldr % 4 || !a.R)
     return hipErrorInvalidValue;
   if (a.C8 && (!a.C2 || !a.C8s || !a.ss8 || a.ldc != a.N)) return hipErrorInvalidValue;
-  switch (bm > 0 ? bm : gemm_rp_panel_rows(a.M)) {
-    case 16: return launch_rp<1, 1>(a, st);
-    case 32: return launch_rp<1, 2>(a, st);
-    case 48: return launch_rp<1, 3>(a, st);
-    case 64: return launch_rp<1, 4>(a, st);
-    case 80: return launch_rp<1, 5>(a, st);
-    case 96: return launch_rp<2, 3>(a, st);
-    case 128: return launch_rp<2, 4>(a, st);
-    case 160: return launch_rp<2, 5>(a, st);
-    default: return hipErrorInvalidValue;
-  }
+  RpArgs r{};
+  r.A = a.A; r.lda = a.lda; r.W = a.W; r.bias = a.bias; r.R = a.R; r.ldr = a.ldr; r.C = a.C; r.ldc = a.ldc;
+  r.C2 = a.C2; r.C8 = a.C8; r.C8s = a.C8s; r.ss8 = a.ss8; r.norm_w = a.norm_w; r.alpha = a.alpha;
+  r.M = a.M; r.K = a.K; r.dbg = a.dbg;
+  return launch_rp_bm<false>(r, bm, st);
+}
+
+hipError_t gemm_rp_mx(const MxArgs& a, const float* norm_w, hipStream_t st, int bm) {
+  // RESID with the fp16 residual stream; the optional MXFP8 operand (Q8) needs the shadow and whole rows
+  if (a.N != kRpN || a.K % 128 || a.K < 128 || a.M <= 0 || !a.res16 || !a.R || a.c_bf16 || a.lda % 16 ||
+      a.ldas != a.K / 32 || a.ldc % 8 || a.ldr % 4 || (int64_t)a.M * a.lda >= (1ll << 32))
+    return hipErrorInvalidValue;
+  if (a.Q8 && (!a.C2 || !a.Q8s || !a.ss8 || a.ldc != a.N)) return hipErrorInvalidValue;
+  RpArgs r{};
+  r.A = a.A; r.lda = a.lda; r.As = a.As; r.ldas = a.ldas; r.W = a.W; r.Ws = a.Ws; r.bias = a.bias; r.R = a.R;
+  r.ldr = a.ldr; r.C = a.C; r.ldc = a.ldc; r.C2 = a.C2; r.C8 = a.Q8; r.C8s = a.Q8s; r.ss8 = a.ss8; r.norm_w = norm_w;
+  r.alpha = a.alpha; r.M = a.M; r.K = a.K; r.dbg = a.dbg;
+  return launch_rp_bm<true>(r, bm, st);
 }
 
 }  // namespace tone

@@ -132,6 +132,9 @@ struct MxArgs {
   int dbg;                // microbenchmarks only (gemm_mx.hip DBG bits); 0 in the session
 };
 hipError_t gemm_mx(const MxArgs& a, int epi, hipStream_t st);
+// the row-panel residual GEMM (gemm_rp.hip) on MXFP8 operands: RESID, N = 384, fp16 residual, optional fused RMSNorm
+// (norm_w) and MXFP8 form of the shadow (a.Q8); bm = panel rows (0: about one panel per CU)
+hipError_t gemm_rp_mx(const MxArgs& a, const float* norm_w, hipStream_t st, int bm = 0);
 // X-stationary MXFP8 GEMM for K = 384 (gemm_mx.hip gemm_xs8_kernel): SWIGLU (-> MXFP8 h) / STORE (bf16 out)
 hipError_t gemm_xs8(const MxArgs& a, int epi, int nc, hipStream_t st);
 // bf16 [M][K] (ldx elements) -> e4m3 [M][K] + E8M0 [M][K/32]; ss8 (optional): the rows' sum-of-squares slab

@@ -439,7 +439,7 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
 int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8, const uint8_t* As, const MxW& w, void* C,
             int64_t ldc, const float* bias, int M, int N, int K, int epi, const float* rs_ss, const float* R = nullptr,
             float alpha = 1.0f, bool c_bf16 = false, uint16_t* C2 = nullptr, uint8_t* C8 = nullptr,
-            uint8_t* C8s = nullptr, bool mx_out = false) {
+            uint8_t* C8s = nullptr, bool mx_out = false, const float* norm_w = nullptr) {
   MxArgs a{};
   a.A = A8;
   a.lda = K;
@@ -474,6 +474,12 @@ int mx_call(tone_session* s, hipStream_t st, const char* fam, const uint8_t* A8,
     LAUNCH(fam, gemm_xs8(a, epi, 0, st));
     return TONE_OK;
   }
+  // the residual-output projections at large M: whole rows per workgroup (gemm_rp.hip; optionally the fused norm)
+  if (epi == EPI_RESID && N == kD && gemm_rp_routed(M, K)) {
+    LAUNCH(fam, gemm_rp_mx(a, norm_w, st));
+    return TONE_OK;
+  }
+  if (norm_w) return fail(TONE_E_HIP, std::string(fam) + ": a fused norm needs the row-panel route");
   LAUNCH(fam, gemm_mx(a, epi, st));
   return TONE_OK;
 }
@@ -532,8 +538,10 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     const LayerW& w = s->L[l];
     const int M = B * T;
     const void* xa = bf ? static_cast<const void*>(xs) : x;   // A operand of the rowscale GEMMs
-    // bf16 mode: norm_out runs inside FFN2's down-projection when that launch is a row-panel one (whole rows)
-    const bool norm_fused = bf && !f8 && knobs().rp_norm && gemm_rp_routed(M, kDff);
+    // bf16 / fp8 modes: norm_out runs inside FFN2's down-projection when that launch is a row-panel one (whole rows);
+    // in fp8 mode it then also emits the next layer's FFN1 operand
+    const bool norm_fused = bf && knobs().rp_norm && gemm_rp_routed(M, kDff);
+    const bool q8_after_norm = f8n && l != 6 && l < 14;
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
     // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
     // up-projection's epilogue
@@ -546,8 +554,9 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
         CALL(mx_call(s, st, "gemm_ffn_up", s->a8, s->a8s, w.mx13[f], nullptr, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU,
                      s->ss8, nullptr, 1.0f, false, nullptr, s->h8, s->h8s));
         q8_fresh = f8n && f == 0 && l < 14;   // FFN1 down emits the MXFP8 operand of layers 0-13's q|k|v
+        const bool fuse = f == 1 && norm_fused;   // FFN2 down + norm_out: the operand of the next layer's FFN1
         return mx_call(s, st, "gemm_ffn_down", s->h8, s->h8s, w.mx2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, nullptr, x,
-                       0.5f, false, xs, nullptr, nullptr, q8_fresh);
+                       0.5f, false, xs, nullptr, nullptr, fuse ? q8_after_norm : q8_fresh, fuse ? w.norm_out : nullptr);
       }
       CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[f], s->h, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
                      1.0f, true, true));
@@ -649,7 +658,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     // FFN2 + norm_out (conformer_blocks.py:832-836)
     CALL(ffn(1));
     // the next layer's FFN1 reads this norm's output unless the reduction / upsampling comes in between
-    q8_fresh = f8n && l != 6 && l < 14;
+    q8_fresh = q8_after_norm;
     if (!norm_fused)
       LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, bf, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->ss8));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual

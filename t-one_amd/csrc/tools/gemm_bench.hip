@@ -133,10 +133,14 @@ __global__ void ss_to_inv_kernel(const float* ss8, float* inv, int M) {
 }
 
 static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, const float* R, float* ref, float* err,
-                   int M, int N, int K, int epi, int rowscale, int iters, int xs = 0) {
+                   int M, int N, int K, int epi, int rowscale, int iters, int xs = 0, const __half* R16 = nullptr) {
   // xs: 98 = the X-stationary kernel (gemm_xs8, SWIGLU only; XSNC = W tiles per item, 0 auto)
   const int xsnc = getenv("XSNC") ? atoi(getenv("XSNC")) : 0;
-  auto mx = [&](const MxArgs& a) { return xs ? gemm_xs8(a, epi, xsnc, 0) : gemm_mx(a, epi, 0); };
+  // RPMX=1 (RESID, with RES16): the row-panel kernel on MXFP8 operands (gemm_rp_mx) instead of gemm_mx
+  const int rpmx = getenv("RPMX") ? atoi(getenv("RPMX")) : 0;
+  auto mx = [&](const MxArgs& a) {
+    return xs ? gemm_xs8(a, epi, xsnc, 0) : (rpmx && epi == 1) ? gemm_rp_mx(a, nullptr, 0) : gemm_mx(a, epi, 0);
+  };
   const int nout = epi >= 2 ? N / 2 : N;
   uint8_t *A8, *As, *W8, *Ws, *C8, *C8s;
   float *inv, *ss8, *Af, *Wf, *C, *Cf;
@@ -162,7 +166,9 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   }
   MxArgs a{};
   a.A = A8p; a.lda = K + pad; a.As = As; a.ldas = K / 32; a.W = W8; a.Ws = Ws; a.rs_ss = rowscale ? ss8 : nullptr;
-  a.bias = bias; a.C = C; a.ldc = nout; a.c_bf16 = 0; a.R = R; a.ldr = N; a.alpha = 1.f;
+  a.bias = bias; a.C = C; a.ldc = nout; a.c_bf16 = 0; a.R = R16 ? reinterpret_cast<const float*>(R16) : R; a.ldr = N;
+  a.alpha = 1.f;
+  a.res16 = R16 != nullptr && epi == 1;
   a.C8 = C8; a.C8s = C8s; a.ldc8s = nout / 32; a.M = M; a.N = N; a.K = K;
   a.dbg = getenv("MXDBG") ? atoi(getenv("MXDBG")) : 0;   // gemm_mx.hip DBG bits (SWIGLU only)
   if (epi >= 2) a.ldc = nout;   // bytes of C8 rows
@@ -175,7 +181,7 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
     chk = Cf;
   }
   CK(hipMemset(err, 0, 4));
-  hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)chk, 0, ref, (int64_t)M * nout, err);
+  hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)chk, a.res16 ? 2 : 0, ref, (int64_t)M * nout, err);
   float herr;
   CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
   hipEvent_t e0, e1;
@@ -306,7 +312,7 @@ int main(int argc, char** argv) {
   for (char* tok = strtok(list, ","); tok; tok = strtok(nullptr, ",")) {
     const int vv = atoi(tok);
     if (vv == 99 || vv == 98) {   // MXFP8 path: quant_mx + gemm_mx (99) / gemm_xs8 (98) vs an fp64 reference
-      run_mx(A, W, bias, R, ref, err, M, N, K, epi, rowscale, iters, vv == 98);
+      run_mx(A, W, bias, R, ref, err, M, N, K, epi, rowscale, iters, vv == 98, res16 ? R16 : nullptr);
       continue;
     }
     // v % 100 = variant (20..23: gemm_t tiles); (v / 100) bits: 1 N-partitioned XCD order,
