@@ -9,7 +9,7 @@ C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 for d in 0 1 2 3; do
   o=gpurun_out/xs8_pmc_$d
   rm -rf $o
-  ROWSCALE=1 MXDBG=$d timeout -s KILL 60 rocprofv3 --pmc $C -d $o -o run --output-format csv -- $A 40960 384 3072 2 98 1 5 > $o.log 2>&1 || exit $?
+  NOREF=1 ROWSCALE=1 MXDBG=$d timeout -s KILL 60 rocprofv3 --pmc $C -d $o -o run --output-format csv -- $A 40960 384 3072 2 98 1 5 > $o.log 2>&1 || exit $?
   echo "dbg $d ok"; grep variant $o.log | tail -1
 done
 python3 - <<'PY'

@@ -155,8 +155,11 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   CK(launch_quant_mx(W, K, N, K, W8, Ws, nullptr, 0));
   hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)M * K + 255) / 256)), dim3(256), 0, 0, A8, As, Af, (int64_t)M, K);
   hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)N * K + 255) / 256)), dim3(256), 0, 0, W8, Ws, Wf, (int64_t)N, K);
-  hipLaunchKernelGGL(ref_mx_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, Af, Wf, bias, R, rowscale ? inv : nullptr,
-                     ref, M, N, K, epi);
+  // NOREF=1: no fp64 reference (timing / counter runs: under rocprofv3 --pmc the naive reference takes minutes)
+  const bool noref = getenv("NOREF") && atoi(getenv("NOREF"));
+  if (!noref)
+    hipLaunchKernelGGL(ref_mx_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, Af, Wf, bias, R, rowscale ? inv : nullptr,
+                       ref, M, N, K, epi);
   // LDAPAD: X rows at a pitch of K + LDAPAD bytes (L2 channel spread of the row-strided K-tile reads)
   const int pad = getenv("LDAPAD") ? atoi(getenv("LDAPAD")) : 0;
   uint8_t* A8p = A8;
