@@ -198,7 +198,7 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / iters;
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK(launch_quant_mx(A, K, M, K, A8, As, rowscale ? inv : nullptr, 0));
+  for (int i = 0; i < iters; ++i) CK(launch_quant_mx(A, K, M, K, A8, As, rowscale ? ss8 : nullptr, 0));   // the slab: M x kSsSlots
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float qms;
