@@ -630,8 +630,9 @@ def test_hip_vs_exported_fp16_graph(sess):
 
 
 # bf16 / fp8 modes against the exported fp16 graph (golden_fp16.npz): both keep the residual stream in fp16 as that
-# graph does.  Measured on the MI355X (profiles/r05_fp16_graph_lowprec.txt): bounds about 1.5x the measured max / mean.
-FP16_GRAPH_BOUNDS = {"bf16": (0.1, 0.02), "fp8": (0.6, 0.1)}
+# graph does.  Measured on the MI355X (profiles/r05_lowprec_bounds.log): bf16 max 0.051 / mean 0.0105 / 0 argmax
+# flips of 480 frames, fp8 max 0.42 / mean 0.088 / 1 flip; bounds about 1.5x the measured max / mean.
+FP16_GRAPH_BOUNDS = {"bf16": (0.08, 0.016), "fp8": (0.6, 0.13)}
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp8"])
