@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of two library builds: TONEHIP_LIB=t-one_amd/libtonehip_base.so (A, ${BASE:-round-5 start}) vs the tree's
+# A/B of two library builds: TONEHIP_LIB=${BASE_LIB:-t-one_amd/libtonehip_base.so} (A, round-5 start by default) vs the tree's
 # libtonehip.so (B), alternating, one bench process per leg; LEGS="precision batch [chunk];..."
 # -> gpurun_out/r05_ab_<tag>.jsonl
 set -u
@@ -12,7 +12,7 @@ for rep in 1 2; do
   for leg in "${legs[@]}"; do
     set -- $leg
     for lib in base cur; do
-      if [ $lib = base ]; then export TONEHIP_LIB=t-one_amd/libtonehip_base.so; else unset TONEHIP_LIB; fi
+      if [ $lib = base ]; then export TONEHIP_LIB=${BASE_LIB:-t-one_amd/libtonehip_base.so}; else unset TONEHIP_LIB; fi
       timeout -k 10 240 python bench.py --precision $1 --batch $2 --steps ${STEPS:-150} --warmup 3 --alt 0 --config4 0 --config5 0 \
         --chunk-samples ${3:-2400} --cpu-baseline-s 0 --detail gpurun_out/ab_detail.json > gpurun_out/ab_leg.json 2> gpurun_out/ab_leg.err || { tail -5 gpurun_out/ab_leg.err; exit 1; }
       python3 -c "

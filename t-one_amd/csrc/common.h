@@ -176,6 +176,21 @@ __device__ __forceinline__ void ring_wait(int j, int n) {
   else vmcnt_dyn(c);
 }
 
+// reductions over the four lanes l ^ {0, 16, 32, 48} (one value per 16-lane row): v_permlane16_swap then
+// v_permlane32_swap, plain VALU (__shfl_xor's ds_bpermute goes through the LDS and its lgkmcnt(0) also waits for
+// every fragment read in flight).  Same association as v + shfl_xor(v, 16), then + shfl_xor(., 32).
+__device__ __forceinline__ float lg_max(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float lg_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

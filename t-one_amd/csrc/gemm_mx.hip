@@ -280,8 +280,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
           float am = 0.f;
 #pragma unroll
           for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
-          am = fmaxf(am, __shfl_xor(am, 16, 64));
-          am = fmaxf(am, __shfl_xor(am, 32, 64));
+          am = lg_max(am);
           const int e = mx_exp(am);
           const u32x2 qv = quant8(v, exp2i(e));
           const int blk = (n0 >> 1) + (wrow0 >> 1) + 32 * pb;     // first output column of the block
@@ -335,8 +334,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
                   am = fmaxf(am, fabsf(vq[2 * k + h][r]));
                   ssq = fmaf(vq[2 * k + h][r], vq[2 * k + h][r], ssq);
                 }
-              am = fmaxf(am, __shfl_xor(am, 16, 64));
-              am = fmaxf(am, __shfl_xor(am, 32, 64));
+              am = lg_max(am);
               const int e = mx_exp(am);
               const float sc = exp2i(e);
               const int col = n0 + wrow0 + 32 * k + 4 * lg;
@@ -347,8 +345,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
               }
               if (ok && lg == 0) p.Q8s[mrow * (p.ldc / 32) + (n0 + wrow0) / 32 + k] = (uint8_t)e;
             }
-            ssq += __shfl_xor(ssq, 16, 64);
-            ssq += __shfl_xor(ssq, 32, 64);
+            ssq = lg_sum(ssq);
             if (ok && lg == 0) {
 #pragma unroll
               for (int k = 0; k < RW / 32; ++k) p.ss8[mrow * kSsSlots + (n0 + wrow0) / 32 + k] = k == 0 ? ssq : 0.f;
@@ -526,7 +523,8 @@ constexpr int kX8MaxN = 3072;
 
 // DBG (XS8_ABLATE microbenchmark builds only): 1 no epilogue, 2 no MFMA, 4 no W DMA after the prologue, 8 SwiGLU
 // without the MX quantization (raw bits stored), 16 no workgroup barrier per W tile (wrong results: timing only),
-// 32 static priority for waves 4-7, 256 no W fragment reads, 512 no X loads (timing only)
+// 32 static priority for waves 4-7, 256 no W fragment reads, 512 no X loads, 1024 no epilogue stores, 2048 no bias
+// reads (timing only)
 template <int EPI, bool RS, int DBG = 0>
 __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_STORE, "SWIGLU / STORE");
@@ -643,7 +641,8 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           for (int r = 0; r < 4; r += 2) {
             const f32x2 ag = {acc[b][mb][h2][r], acc[b][mb][h2][r + 1]};
             const f32x2 au = {acc[b][mb][2 + h2][r], acc[b][mb][2 + h2][r + 1]};
-            const f32x2 bg = {sb[ng + r], sb[ng + r + 1]}, bu = {sb[ng + 32 + r], sb[ng + 33 + r]};
+            f32x2 bg = {sb[ng + r], sb[ng + r + 1]}, bu = {sb[ng + 32 + r], sb[ng + 33 + r]};
+            if constexpr ((DBG & 2048) != 0) { bg = f32x2{0.f, 0.f}; bu = bg; }   // no bias reads (timing only)
             const f32x2 gg = __builtin_elementwise_fma(ag, inv2, bg);
             const f32x2 uu = __builtin_elementwise_fma(au, inv2, bu);
             const f32x2 tt = gg * -1.4426950408889634f;
@@ -661,16 +660,19 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
         } else {
 #pragma unroll
           for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
-          am = fmaxf(am, __shfl_xor(am, 16, 64));
-          am = fmaxf(am, __shfl_xor(am, 32, 64));
+          am = lg_max(am);
           e = mx_exp(am);
           qv = quant8(v, exp2i(e));
         }
         const int col = 32 * t;                                   // first h column of the block
         uint8_t* c8 = p.C8 + orow[mb] + (col + 4 * lg);
-        *reinterpret_cast<uint32_t*>(c8) = qv[0];
-        *reinterpret_cast<uint32_t*>(c8 + 16) = qv[1];
-        p.C8s[srow[mb] + t] = (uint8_t)e;                         // the 4 lanes of the block write the same byte
+        if constexpr ((DBG & 1024) != 0) {   // no stores (timing only; the ring wait then counts ops that do not exist)
+          asm volatile("" ::"v"(qv[0]), "v"(qv[1]), "v"(e), "v"(c8));
+        } else {
+          *reinterpret_cast<uint32_t*>(c8) = qv[0];
+          *reinterpret_cast<uint32_t*>(c8 + 16) = qv[1];
+          p.C8s[srow[mb] + t] = (uint8_t)e;                       // the 4 lanes of the block write the same byte
+        }
       } else {
 #pragma unroll
         for (int nb2 = 0; nb2 < 2; ++nb2) {
@@ -736,8 +738,12 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
     // previous tile's epilogue) are unchanged, so ring_younger's count holds.
     i32x8 wslot[2][4];
     int sslot[2][4];
-    auto tile = [&](auto Bc, int j) __attribute__((always_inline)) {
+    // The first tile of a run is its own instantiation (FIRST: no deferred K-step, no epilogue): with a run-time
+    // `j > 0` around them the compiler sank this tile's K-step 0/1 MFMAs below the branch, i.e. after the whole
+    // epilogue, and the epilogue ran serially (SwiGLU M = 40960: 97 us with it, 53 us without, MFMA at 16 %).
+    auto tile = [&](auto Bc, auto Fc, int j) __attribute__((always_inline)) {
       constexpr int b = decltype(Bc)::value;
+      constexpr bool first = decltype(Fc)::value;
       using PB = std::integral_constant<int, b ^ 1>;
       const int t = t0 + j;
       ring_wait<kX8R, kX8Pieces, kStores8>(j, n);                   // tile t landed
@@ -745,7 +751,7 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (j + kX8R - 1 < n && !(DBG & 4)) dma(t + kX8R - 1);
       rdw(t, 0, wslot[b], sslot[b]);
-      if (j > 0) mstep(PB{}, 2, wslot[b ^ 1], sslot[b ^ 1]);      // the previous tile's deferred K-step
+      if constexpr (!first) mstep(PB{}, 2, wslot[b ^ 1], sslot[b ^ 1]);   // the previous tile's deferred K-step
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
@@ -753,16 +759,23 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
         for (int nb = 0; nb < 4; ++nb) acc[b][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
       rdw(t, 1, wslot[b ^ 1], sslot[b ^ 1]);
       mstep(Bc, 0, wslot[b], sslot[b]);
-      if (j > 0 && !(DBG & 1)) epi_part(b ^ 1, t - 1, 0);         // previous tile, under these MFMAs
+      if constexpr (!first && !(DBG & 1)) epi_part(b ^ 1, t - 1, 0);   // previous tile, under these MFMAs
       __builtin_amdgcn_sched_barrier(0);
       rdw(t, 2, wslot[b], sslot[b]);
       mstep(Bc, 1, wslot[b ^ 1], sslot[b ^ 1]);
-      if (j > 0 && !(DBG & 1)) { epi_part(b ^ 1, t - 1, 2); epi_part(b ^ 1, t - 1, 1); epi_part(b ^ 1, t - 1, 3); }
+      if constexpr (!first && !(DBG & 1)) {
+        epi_part(b ^ 1, t - 1, 2);
+        epi_part(b ^ 1, t - 1, 1);
+        epi_part(b ^ 1, t - 1, 3);
+      }
       __builtin_amdgcn_sched_barrier(0);
     };
-    for (int j = 0; j < n; j += 2) {
-      tile(std::integral_constant<int, 0>{}, j);
-      if (j + 1 < n) tile(std::integral_constant<int, 1>{}, j + 1);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    tile(I0{}, std::true_type{}, 0);
+    for (int j = 1; j < n; j += 2) {
+      tile(I1{}, std::false_type{}, j);
+      if (j + 1 < n) tile(I0{}, std::false_type{}, j + 1);
     }
     // the last tile: its deferred K-step, then its epilogue
     auto drain = [&](auto Bc) __attribute__((always_inline)) {
@@ -797,6 +810,7 @@ hipError_t launch_xs8(const MxArgs& a, int nc, hipStream_t st) {
     switch (a.rs_ss ? a.dbg : 0) {
 #define X8_D(d) case d: hipLaunchKernelGGL((gemm_xs8_kernel<EPI, true, d>), dim3(grid), dim3(512), 0, st, a, nc); return hipGetLastError();
       X8_D(1) X8_D(2) X8_D(3) X8_D(4) X8_D(5) X8_D(8) X8_D(7) X8_D(16) X8_D(17) X8_D(32) X8_D(20) X8_D(259) X8_D(515) X8_D(771) X8_D(263) X8_D(19) X8_D(256) X8_D(512)
+      X8_D(1024) X8_D(2048) X8_D(3072) X8_D(1032) X8_D(1026)
 #undef X8_D
       default: break;
     }
