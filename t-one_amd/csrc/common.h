@@ -191,6 +191,21 @@ __device__ __forceinline__ float lg_sum(float v) {
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
+// max |v| over 8 values and the lane group, as the bits of a non-negative float: the lane's own values by fmaxf, the
+// lane swaps by integer max on the bits (finite and infinite magnitudes order like their bit patterns), which saves the
+// canonicalizing v_max_f32 x, x, x fmaxf needs after every swap.  Identical to the all-fmaxf form unless a lane's own 8
+// values are all NaN (fmaxf drops a NaN beside a number; that lane's NaN bits win the integer max); the NaN values stay
+// NaN through quant4 either way
+__device__ __forceinline__ uint32_t lg_max_abs_bits(const float (&v)[8]) {
+  float f = 0.f;   // the lane's own 8 values: v_max3_f32 with |.| source modifiers
+#pragma unroll
+  for (int r = 0; r < 8; ++r) f = fmaxf(f, fabsf(v[r]));
+  uint32_t m = __float_as_uint(f);
+  const auto a = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+  m = max((uint32_t)a[0], (uint32_t)a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+  return max((uint32_t)b[0], (uint32_t)b[1]);
+}
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

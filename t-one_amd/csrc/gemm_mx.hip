@@ -529,9 +529,13 @@ template <int EPI, bool RS, int DBG = 0>
 __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_STORE, "SWIGLU / STORE");
   constexpr int kStores8 = EPI == EPI_SWIGLU ? 2 * 3 : 4 * 2;      // vector stores per tile epilogue (per lane)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kX8R * kX8Tile + kX8MaxN * (kX8K / 32) + 4 * kX8MaxN];
-  uint8_t* sWs = lds + kX8R * kX8Tile;                         // W scales [N][12]
+  // W scales [N][12] and bias first, the ring after them: every per-tile scale read is then a per-tile base plus an
+  // immediate below 64 KiB (behind a 96 KiB ring each of the 12 scale reads of a tile took its own address add)
+  constexpr int kRingOff = kX8MaxN * (kX8K / 32) + 4 * kX8MaxN;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRingOff + kX8R * kX8Tile];
+  uint8_t* sWs = lds;
   float* sb = reinterpret_cast<float*>(sWs + kX8MaxN * (kX8K / 32));
+  uint8_t* ring = lds + kRingOff;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lg = lane >> 4, swz = (l15 >> 1) & 7;
@@ -569,20 +573,23 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
   }
   __syncthreads();                                                // no DMA in flight yet
 
+  // the lane's byte offset in a W tile for each of its DMA pieces, computed once (32-bit: three VGPRs; recomputed per
+  // tile the division by 24 and its multiplies were ~35 VALU of the tile's VALU-bound epilogue budget)
+  uint32_t doff[kX8Pieces];
+#pragma unroll
+  for (int i = 0; i < kX8Pieces; ++i) {
+    const int pc = wid * kX8Pieces + i, lin = pc * 64 + lane, row = lin / 24, slot = lin % 24;
+    doff[i] = (uint32_t)(row * kX8K + ((slot ^ ((row >> 1) & 7)) << 4));
+  }
   auto dma = [&](int t) {
-    uint8_t* base = lds + (t % kX8R) * kX8Tile;
+    uint8_t* base = ring + (t % kX8R) * kX8Tile;
     (void)base;
     const uint8_t* wt = p.W + (int64_t)t * kX8Tile;               // uniform: the tile's first W row
-    // the lane's piece addresses are recomputed per call (a few VALU): hoisted out of the tile loop they were three
-    // 64-bit pointers the register allocator spilled, and every scratch reload drained vmcnt
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int i = 0; i < kX8Pieces; ++i) {
-      const int pc = wid * kX8Pieces + i, lin = pc * 64 + ln, row = lin / 24, slot = lin % 24;
-      const uint8_t* src = wt + (uint32_t)(row * kX8K + ((slot ^ ((row >> 1) & 7)) << 4));
+      const uint8_t* src = wt + doff[i];
 #if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + pc * 1024, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, base + (wid * kX8Pieces + i) * 1024, 16, 0, 0);
 #else
       (void)src;
 #endif
@@ -630,38 +637,28 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       const int mb = part >> 1, hh = part & 1;
       if constexpr (EPI == EPI_SWIGLU) {
         if (hh) return;                       // one MX block (32 h columns) per row and tile: both halves here
-        // value pairs as two-float vectors so the fused multiply-adds and products issue as v_pk_* (the same
-        // per-element roundings as the scalar form)
+        // scalar fp32 (packed f32 VALU beside MFMAs costs more issue time than two plain ops, MI355X_MICROARCH.md
+        // constants table; the file is built with -fno-slp-vectorize so these stay scalar)
         float v[8];
-        const f32x2 inv2 = {inv[mb], inv[mb]};
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
           const int ng = kX8BN * t + 16 * h2 + 4 * lg;
 #pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            const f32x2 ag = {acc[b][mb][h2][r], acc[b][mb][h2][r + 1]};
-            const f32x2 au = {acc[b][mb][2 + h2][r], acc[b][mb][2 + h2][r + 1]};
-            f32x2 bg = {sb[ng + r], sb[ng + r + 1]}, bu = {sb[ng + 32 + r], sb[ng + 33 + r]};
-            if constexpr ((DBG & 2048) != 0) { bg = f32x2{0.f, 0.f}; bu = bg; }   // no bias reads (timing only)
-            const f32x2 gg = __builtin_elementwise_fma(ag, inv2, bg);
-            const f32x2 uu = __builtin_elementwise_fma(au, inv2, bu);
-            const f32x2 tt = gg * -1.4426950408889634f;
-            const f32x2 dd = f32x2{__builtin_amdgcn_exp2f(tt.x), __builtin_amdgcn_exp2f(tt.y)} + 1.0f;
-            const f32x2 oo = gg * f32x2{__builtin_amdgcn_rcpf(dd.x), __builtin_amdgcn_rcpf(dd.y)} * uu;
-            v[4 * h2 + r] = oo.x;
-            v[4 * h2 + r + 1] = oo.y;
+          for (int r = 0; r < 4; ++r) {
+            float bg = sb[ng + r], bu = sb[ng + 32 + r];
+            if constexpr ((DBG & 2048) != 0) { bg = 0.f; bu = 0.f; }   // no bias reads (timing only)
+            const float g = fmaf(acc[b][mb][h2][r], inv[mb], bg);
+            const float u = fmaf(acc[b][mb][2 + h2][r], inv[mb], bu);
+            const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g * -1.4426950408889634f));
+            v[4 * h2 + r] = g * sg * u;
           }
         }
-        float am = 0.f;
         int e = 0;
         u32x2 qv;
         if constexpr (DBG & 8) {
           qv = u32x2{__float_as_uint(v[0] + v[1] + v[2] + v[3]), __float_as_uint(v[4] + v[5] + v[6] + v[7])};
         } else {
-#pragma unroll
-          for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
-          am = lg_max(am);
-          e = mx_exp(am);
+          e = mx_exp(__uint_as_float(lg_max_abs_bits(v)));
           qv = quant8(v, exp2i(e));
         }
         const int col = 32 * t;                                   // first h column of the block
@@ -704,8 +701,8 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       }
       // (8 ks + c) ^ swz = 8 ks + (c ^ swz) for swz < 8: one lane-constant address per half plus compile-time offsets
       // (n-block, K-step) that fold into the ds_read immediates; the ring slot and the tile's scale rows are uniform
-      const uint8_t* b0 = lds + (t % kX8R) * kX8Tile + xa0;
-      const uint8_t* b1 = lds + (t % kX8R) * kX8Tile + xa1;
+      const uint8_t* b0 = ring + (t % kX8R) * kX8Tile + xa0;
+      const uint8_t* b1 = ring + (t % kX8R) * kX8Tile + xa1;
       const uint8_t* bs = sWs + t * kX8BN * (kX8K / 32) + xas;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
