@@ -42,7 +42,12 @@ __device__ __forceinline__ float fast_sigmoid(float x) {
 __device__ __forceinline__ float fast_silu(float x) { return x * fast_sigmoid(x); }
 
 __device__ __forceinline__ void barrier_lds() {   // keeps LDS-DMA in flight (no vmcnt(0) fence)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // lgkmcnt(0) (vmcnt / expcnt at their maxima) as the builtin, so the compiler's wait-count pass knows every earlier
+  // LDS read has completed: written as inline asm it was opaque to the pass, which then put a second lgkmcnt(0) in
+  // front of the first use of a fragment read before the barrier -- and that one also drained every read issued
+  // after the barrier (gemm_xs8: its deferred K-step waited on the next K-step's fragments and the bias)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
 }
 

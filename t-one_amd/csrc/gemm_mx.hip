@@ -633,6 +633,14 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       orow[mb] = mrow * (uint32_t)p.ldc;
       srow[mb] = mrow * (uint32_t)p.ldc8s;
     }
+    // SwiGLU bias of the tile whose epilogue runs next: its 16 values per lane (g and u, columns 16 h2 + 4 lg + r) are
+    // read at the top of the tile, ahead of the fragment reads, so the epilogue's first use waits on these four reads
+    // only (read inside the epilogue, their lgkmcnt wait also drained the K-step's fragment reads issued before them)
+    f32x4 bias4[4];
+    auto fetch_bias = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bias4[q] = *reinterpret_cast<const f32x4*>(sb + kX8BN * t + 16 * (q & 1) + 32 * (q >> 1) + 4 * lg);
+    };
     auto epi_part = [&](int b, int t, int part) __attribute__((always_inline)) {
       const int mb = part >> 1, hh = part & 1;
       if constexpr (EPI == EPI_SWIGLU) {
@@ -642,11 +650,10 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
         float v[8];
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
-          const int ng = kX8BN * t + 16 * h2 + 4 * lg;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float bg = sb[ng + r], bu = sb[ng + 32 + r];
-            if constexpr ((DBG & 2048) != 0) { bg = 0.f; bu = 0.f; }   // no bias reads (timing only)
+            float bg = bias4[h2][r], bu = bias4[2 + h2][r];
+            if constexpr ((DBG & 2048) != 0) { bg = 0.f; bu = 0.f; }   // no bias (timing only)
             const float g = fmaf(acc[b][mb][h2][r], inv[mb], bg);
             const float u = fmaf(acc[b][mb][2 + h2][r], inv[mb], bu);
             const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g * -1.4426950408889634f));
@@ -747,8 +754,9 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
       if constexpr (!(DBG & 16)) barrier_lds();                   // ... for every wave; slot (t - 1) % R free
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (j + kX8R - 1 < n && !(DBG & 4)) dma(t + kX8R - 1);
-      rdw(t, 0, wslot[b], sslot[b]);
       if constexpr (!first) mstep(PB{}, 2, wslot[b ^ 1], sslot[b ^ 1]);   // the previous tile's deferred K-step
+      if constexpr (EPI == EPI_SWIGLU && !first) fetch_bias(t - 1);
+      rdw(t, 0, wslot[b], sslot[b]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
@@ -786,6 +794,7 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           for (int nb = 0; nb < 4; ++nb) k += acc[0][mb][nb][0] + acc[1][mb][nb][1];
         if (k == 1234.5f) p.C8[mbase] = 1;
       } else {
+        if constexpr (EPI == EPI_SWIGLU) fetch_bias(t1 - 1);
 #pragma unroll
         for (int part = 0; part < 4; ++part) epi_part(b, t1 - 1, part);
       }
