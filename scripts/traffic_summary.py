@@ -13,9 +13,10 @@ UP = {  # SWIGLU instantiations: EPI_SWIGLU = 2
     "bf16": r"(gemm_t_kernel<tone::(?:\(anonymous namespace\)::)?TT<[^>]*>, 2,|gemm_x[sw]\d?_kernel<2, )",
     "fp8": r"(gemm_xs8_kernel<2, |gemm_mx_kernel<\d+, 2, )",
 }[prec]
-# EPI_RESID = 1, in any GEMM kernel family
+# EPI_RESID = 1, in any GEMM kernel family; every gemm_rp_kernel launch
 RESID = (r"(gemm_x3_kernel<tone::(?:\(anonymous namespace\)::)?XT<[^>]*>, 1,|gemm_glds_kernel<tone::(?:\(anonymous namespace\)::)?Tile<[^>]*>, 1,|gemm_kernel<tone::(?:\(anonymous namespace\)::)?Tile<[^>]*>, 1,"
-         r"|gemm_t_kernel<tone::(?:\(anonymous namespace\)::)?TT<[^>]*>, 1,|gemm_f32t_kernel<[^>]*>, 1,|gemm_mx_kernel<\d+, 1,)")
+         r"|gemm_t_kernel<tone::(?:\(anonymous namespace\)::)?TT<[^>]*>, 1,|gemm_f32t_kernel<[^>]*>, 1,|gemm_mx_kernel<\d+, 1,"
+         r"|gemm_rp_kernel<)")   # the row-panel kernel (round 5) is RESID only
 
 
 def per_launch(sub, pat):
