@@ -1058,6 +1058,19 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
       // K = 384 projections (8.1 vs 11.1 us) (scripts/x3n_sweep.sh, profiles/r01_x3n_sweep_b256.jsonl); past one per
       // CU the 64x64 tile (M = 1536, the 400 ms reduced layers: FFN down 28.4 vs 34.3 us, K = 384 10.9 vs 13.8)
       return gemm_x3(a, epi, 10, st);
+    // N = 384, K = 1536 (FFN down) where the 64x64 tiles miss one full round of the CUs -- 312 of them at M = 3328 (the
+    // 400 ms full layers: 1.22 rounds), 144 at M = 1536 (the 400 ms reduced layers) -- a 3-way K split on 128x128 /
+    // 64W x 128X tiles (234 / 216 workgroups, partials reduced in a fixed order by splitk_epilogue): 36.4 vs 54.5 us and
+    // 23.8 vs 28.2; at M = 2560 (240 tiles) the split is no faster (scripts/r05_x3_splitk.sh,
+    // profiles/r05_x3_splitk.jsonl)
+    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N == 384 && a.K == 1536 && !a.rowscale && a.ws && !a.c_plane &&
+        !a.c2_plane && (int64_t)3 * a.M * a.N <= a.ws_cap) {
+      const int64_t t0 = (int64_t)((a.M + 63) / 64) * (a.N / 64);
+      if ((t0 > 256 || t0 < 192) && a.M <= 4096) {   // measured up to M = 3328
+        const hipError_t e = gemm_x3_splitk(a, epi, a.M >= 2048 ? 6 : 2, 3, st);
+        if (e != hipErrorInvalidValue) return e;
+      }
+    }
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_x3(a, epi, 0, st);
   }
   if (!bf16 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
