@@ -1047,7 +1047,10 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
       return gemm_x3(a, epi, (t8 > 128 && t8 <= 256) ? 8 : 6, st);
     }
     if (epi == EPI_SWIGLU && a.N % 128 == 0) return gemm_x3(a, epi, 6, st);
-    if (epi == EPI_GLU && a.N % 128 == 0) return gemm_x3(a, epi, 1, st);
+    // pw1: 128 W x 64 X tiles, or 128 x 128 once those overflow one round of the CUs (M = 3328, the 400 ms full layers:
+    // 312 vs 156 workgroups, 22.1 vs 26.4 us; scripts/r05_x3_400.sh, profiles/r05_x3_400.jsonl)
+    if (epi == EPI_GLU && a.N % 128 == 0)
+      return gemm_x3(a, epi, ((int64_t)((a.M + 63) / 64) * (a.N / 128) > 256 && a.M <= 4096) ? 6 : 1, st);
     // q|k|v (N = 1152): 128 W x 64 X tiles below ~128 tiles of 128 x 128 (M = 1280 / 1536: 15.5 / 16.3 vs 22.7 / 23.1 us)
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N >= 1024 && a.N % 128 == 0)
       return gemm_x3(a, epi, (int64_t)((a.M + 127) / 128) * (a.N / 128) < 128 ? 1 : 6, st);
@@ -1071,6 +1074,11 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
         if (e != hipErrorInvalidValue) return e;
       }
     }
+    // K = 384 at M = 3328 (attn-out / pw2 of the 400 ms full layers): the 64x64 tiles make 1.22 rounds, 128 W x 64 X
+    // tiles one (15.8 vs 20.8 us, profiles/r05_x3_400.jsonl)
+    if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 128 == 0 && a.K == 384 && a.M <= 4096 &&
+        (int64_t)((a.M + 63) / 64) * (a.N / 64) > 256)
+      return gemm_x3(a, epi, 1, st);
     if ((epi == EPI_STORE || epi == EPI_RESID) && a.N % 64 == 0) return gemm_x3(a, epi, 0, st);
   }
   if (!bf16 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
