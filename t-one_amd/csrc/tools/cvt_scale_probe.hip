@@ -1,0 +1,66 @@
+// What v_cvt_scalef32_pk_fp8_f32 does with its scale operand (gfx950): for MXFP8 blocks of random values, the bytes of
+// (a) quant4 (x * 2^-E, NaN-keeping clamp to +-448, v_cvt_pk_fp8_f32) against (b) the scaled conversion of x clamped
+// in the unscaled domain (+-448 * 2^E), with the scale operand 2^E and 2^-E.  Prints mismatch counts per variant.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include "../common.h"
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__global__ void probe(const float* x, unsigned* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (2 * i + 1 >= n) return;
+  const float a = x[2 * i], b = x[2 * i + 1];
+  // block of 32 = 16 threads x 2 values: amax over the 16 lanes of the group
+  float am = fmaxf(fabsf(a), fabsf(b));
+  for (int o = 1; o < 16; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+  const int e = tone::mx_exp(am);
+  const float inv = tone::exp2i(e);                                  // 2^(127 - E), E = e biased
+  const float sc = __uint_as_float((uint32_t)(e) << 23);            // 2^(e - 127): the block scale
+  const unsigned ref = tone::quant4(a, b, 0.f, 0.f, inv) & 0xffff;
+  const float lim = 448.f * sc;
+  const float ca = __builtin_elementwise_minimum(__builtin_elementwise_maximum(a, -lim), lim);
+  const float cb = __builtin_elementwise_minimum(__builtin_elementwise_maximum(b, -lim), lim);
+  s16x2 z = {0, 0};
+  const unsigned v1 = (unsigned)(unsigned short)__builtin_amdgcn_cvt_scalef32_pk_fp8_f32(z, ca, cb, sc, false)[0];
+  const unsigned v2 = (unsigned)(unsigned short)__builtin_amdgcn_cvt_scalef32_pk_fp8_f32(z, ca, cb, inv, false)[0];
+  out[3 * i] = ref;
+  out[3 * i + 1] = v1;
+  out[3 * i + 2] = v2;
+}
+int main() {
+  const int n = 1 << 20;
+  float* h = (float*)malloc(n * 4);
+  srand(1);
+  for (int i = 0; i < n; ++i) {
+    const float u = (rand() + 1.f) / (RAND_MAX + 2.f), w = (rand() + 1.f) / (RAND_MAX + 2.f);
+    const float g = sqrtf(-2.f * logf(u)) * cosf(6.2831853f * w);
+    const int blk = i / 32;
+    h[i] = g * ldexpf(1.f, (blk % 40) - 20);                        // block magnitudes 2^-20 .. 2^19
+    if (blk % 97 == 0 && i % 32 == 5) h[i] = 0.f;
+    if (blk % 53 == 1) h[i] = g * ldexpf(1.f, -118 - (blk % 12));   // amax below 2^-118: block exponent 0
+    if (blk % 89 == 2) h[i] = 0.f;                                  // all-zero block
+    if (blk % 211 == 3 && i % 32 == 7) h[i] = (blk % 2) ? INFINITY : NAN;
+  }
+  float* dx; unsigned* dout;
+  hipMalloc(&dx, n * 4); hipMalloc(&dout, (n / 2) * 3 * 4);
+  hipMemcpy(dx, h, n * 4, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(probe, dim3(n / 2 / 256), dim3(256), 0, 0, dx, dout, n);
+  unsigned* o = (unsigned*)malloc((n / 2) * 3 * 4);
+  hipMemcpy(o, dout, (n / 2) * 3 * 4, hipMemcpyDeviceToHost);
+  long m1 = 0, m2 = 0, m1_small = 0, m1_zero = 0, m1_naninf = 0;
+  int shown = 0;
+  for (int i = 0; i < n / 2; ++i) {
+    const int blk = (2 * i) / 32;
+    if (o[3 * i] != o[3 * i + 1]) {
+      if (blk % 53 == 1) ++m1_small;
+      else if (blk % 89 == 2) ++m1_zero;
+      else if (blk % 211 == 3) ++m1_naninf;
+    }
+    if (o[3 * i] != o[3 * i + 1]) { ++m1; if (shown < 8) { printf("scale=2^E  x=(%g,%g) ref 0x%04x got 0x%04x\n", h[2*i], h[2*i+1], o[3*i], o[3*i+1]); ++shown; } }
+    if (o[3 * i] != o[3 * i + 2]) ++m2;
+  }
+  printf("{\"pairs\": %d, \"mismatch_scale_2^E\": %ld, \"of_which_exponent0_blocks\": %ld, \"zero_blocks\": %ld, "
+         "\"nan_inf_blocks\": %ld, \"mismatch_scale_2^-E\": %ld}\n", n / 2, m1, m1_small, m1_zero, m1_naninf, m2);
+  return 0;
+}
