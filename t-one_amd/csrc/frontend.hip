@@ -585,37 +585,82 @@ __global__ void __launch_bounds__(512) sub_conv_bf16_kernel(const float* __restr
   }
   __syncthreads();
 
-  // conv1 tiles -> slab rows 8..37 (and the new sub2 state)
+  // conv1 tiles -> slab rows 8..37 (and the new sub2 state).  Software-pipelined: tile i + 1's fragment reads and
+  // MFMAs are issued before tile i's BN + SiLU epilogue, so the epilogue's VALU runs under the next tile's matrix work.
+  // Every wave runs 12 steps (90 tiles over 8 waves: waves 2-7 have 11, their 12th repeats tile 89 and writes the same
+  // values wave 1 writes there), so the loop has no tile-count branch for the compiler to sink the MFMAs under.
   __half* st2out = s.out + orow + kOffSub2;
-  for (int tile = wid; tile < kMT * 3; tile += 8) {
+  constexpr int kC1Tiles = kMT * 3, kC1Steps = (kC1Tiles + 7) / 8;
+  auto c1_mma = [&](int tile, f32x4 (&acc)[2]) __attribute__((always_inline)) {
     const int t = tile / 3, f0 = (tile % 3) * 16;
     const int a = f0 + n + 8 * g, q = a & 3;                 // A operand: position f0 + n, k group g
     const uint16_t* arow = xc + q * kF1Copy + t * kX1Cols + (a - q);
-    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // every A fragment of the tile requested before its first MFMA (read one K-step ahead, each pair of MFMAs waited
+    // on its own read)
+    bf16x8 av[kSub1Kt];
 #pragma unroll
     for (int kt = 0; kt < kSub1Kt; ++kt) {
       const uint2 lo = *reinterpret_cast<const uint2*>(arow + kt * kX1Cols);
       const uint2 hi = *reinterpret_cast<const uint2*>(arow + kt * kX1Cols + 4);
-      const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wf[kt][0], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wf[kt][1], acc[1], 0, 0, 0);
+      av[kt] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
     }
-    // D 16x16: lane holds channel 16 nt + n of positions f0 + 4 g + r
+    __builtin_amdgcn_sched_barrier(0);
+    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int c = 16 * nt + n;
+    for (int kt = 0; kt < kSub1Kt; ++kt) {
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[kt], wf[kt][0], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[kt], wf[kt][1], acc[1], 0, 0, 0);
+    }
+  };
+  // D 16x16: lane holds channel 16 nt + n of positions f0 + 4 g + r.  A lane's four positions are all valid or all
+  // past the 44 columns (f0 = 32, g = 3), so one lane predicate covers its eight stores; with a test per element the
+  // compiler sank each value's BN + SiLU chain under its own branch and ran the eight chains one after another
+  // (profiles/r05_subconv_ablate.txt)
+  auto c1_epi = [&](int tile, const f32x4 (&acc)[2]) __attribute__((always_inline)) {
+    const int t = tile / 3, f0 = (tile % 3) * 16;
+    if (f0 + 4 * g < kSub1F) {
+      float y[2][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = f0 + 4 * g + r;
-        const float z = fmaf(acc[nt][r], sc1[c], sh1[c]);   // SiLU via v_exp_f32 / v_rcp_f32 (bf16 output)
-        const float y = z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
-        if (f < kSub1F) {
-          const int p = (kSub2S + t) * kSub1F + f;
-          const __bf16 hy = (__bf16)y;
-          slab16[p * kSub1C + (((c >> 3) ^ c2_swz(p)) << 3) + (c & 7)] = __builtin_bit_cast(uint16_t, hy);
-          if (t >= kMT - kSub2S) st2out[(c * kSub2S + (t - (kMT - kSub2S))) * kSub1F + f] = __float2half_rn(y);
+      for (int nt = 0; nt < 2; ++nt) {
+        const int c = 16 * nt + n;
+        const float s1 = sc1[c], h1 = sh1[c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = fmaf(acc[nt][r], s1, h1);           // SiLU via v_exp_f32 / v_rcp_f32 (bf16 output)
+          y[nt][r] = z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
         }
       }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int c = 16 * nt + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = (kSub2S + t) * kSub1F + f0 + 4 * g + r;
+          const __bf16 hy = (__bf16)y[nt][r];
+          slab16[p * kSub1C + (((c >> 3) ^ c2_swz(p)) << 3) + (c & 7)] = __builtin_bit_cast(uint16_t, hy);
+        }
+      }
+      if (t >= kMT - kSub2S) {                                // the new sub2 state rows (tile-uniform)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st2out[((16 * nt + n) * kSub2S + (t - (kMT - kSub2S))) * kSub1F + f0 + 4 * g + r] = __float2half_rn(y[nt][r]);
+      }
+    }
+  };
+  {
+    f32x4 accA[2], accB[2];
+    c1_mma(wid, accA);
+#pragma unroll 1
+    for (int i = 0; i < kC1Steps; i += 2) {
+      const int t0 = min(wid + 8 * i, kC1Tiles - 1), t1 = min(wid + 8 * (i + 1), kC1Tiles - 1);
+      const int t2 = min(wid + 8 * (i + 2), kC1Tiles - 1);
+      c1_mma(t1, accB);
+      c1_epi(t0, accA);
+      if (i + 2 < kC1Steps) c1_mma(t2, accA);
+      c1_epi(t1, accB);
     }
   }
   __syncthreads();                                        // the slab is complete; ring slots 1-2 are free
