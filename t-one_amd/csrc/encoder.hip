@@ -230,8 +230,7 @@ __global__ void __launch_bounds__(256) attention_rec_kernel(AttnArgs a) {
     float sum = 0.f;
 #pragma unroll
     for (int m = 0; m < 12; ++m) sum += x[m];
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
+    sum = lg_sum(sum);
     const float mu = sum * (1.0f / kDk);
     float var = 0.f;
 #pragma unroll
@@ -239,8 +238,7 @@ __global__ void __launch_bounds__(256) attention_rec_kernel(AttnArgs a) {
       x[m] -= mu;
       var += x[m] * x[m];
     }
-    var += __shfl_xor(var, 16, 64);
-    var += __shfl_xor(var, 32, 64);
+    var = lg_sum(var);
     const float rstd = 1.0f / sqrtf(var * (1.0f / kDk) + kLnEps);
 #pragma unroll
     for (int m = 0; m < 12; ++m) x[m] = x[m] * rstd * lw[m] + lb[m];
@@ -291,8 +289,7 @@ __global__ void __launch_bounds__(256) attention_rec_kernel(AttnArgs a) {
       x[t][rr] = j < TK ? (masked ? -10000.0f : sc) : -INFINITY;
       mx = fmaxf(mx, x[t][rr]);
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = lg_max(mx);
   float sum = 0.f;
 #pragma unroll
   for (int t = 0; t < NJT; ++t)
@@ -302,8 +299,7 @@ __global__ void __launch_bounds__(256) attention_rec_kernel(AttnArgs a) {
       x[t][rr] = j < TK ? expf(x[t][rr] - mx) : 0.f;
       sum += x[t][rr];
     }
-  sum += __shfl_xor(sum, 16, 64);
-  sum += __shfl_xor(sum, 32, 64);
+  sum = lg_sum(sum);   // v_permlane16/32_swap, the same association as the two xor shuffles
   const float rsum = 1.0f / sum;                        // one division per lane, not one per probability
   float* pr = a.probs ? a.probs + (((int64_t)b * kHeads + h) * T + i) * TK : nullptr;
 #pragma unroll

@@ -171,8 +171,7 @@ __global__ void __launch_bounds__(KS * 64) gemm_sm_kernel(GemmArgs p) {
     for (int mb = 0; mb < MB; ++mb) {
       float inv = 1.0f;
       if constexpr (RS) {
-        float t = ss[mb] + __shfl_xor(ss[mb], 16, 64);
-        t += __shfl_xor(t, 32, 64);
+        const float t = lg_sum(ss[mb]);   // v_permlane16/32_swap (the xor-16 / xor-32 shuffles' association)
         inv = 1.0f / (sqrtf(t) * p.inv_sqrt_k + kRmsEps);
       }
       const int m = 16 * mb + l16;
