@@ -808,7 +808,9 @@ __global__ void __launch_bounds__(512) conv2_p3_kernel(const float* __restrict__
   split_rows(0);
 
   const int n = lane & 15, g = lane >> 4;
-  const int ntile = wid + NWV * (KT - 1) < kTiles ? KT : KT - 1;  // wave-uniform
+  // wave-uniform; from this part's own rows, so the short last part at 400 ms (T = 13: 5 + 5 + 3 rows, 7 position tiles)
+  // runs one tile per wave instead of repeating clamped positions
+  const int ntile = wid + NWV * (KT - 1) < (posT + 15) / 16 ? KT : KT - 1;
   int xr[KT], xf[KT];                                              // output row / column of this lane's position
 #pragma unroll
   for (int k = 0; k < KT; ++k) {
