@@ -48,6 +48,7 @@ typedef __bf16 xw_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float xw_f32x16 __attribute__((ext_vector_type(16)));
 typedef float xw_f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 xw_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float xw_f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int xw_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int xw_perm(int r) {   // swap bits 2 and 3 (an involution on 0..31)
@@ -113,11 +114,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   auto dma_piece = [&](int t, int sl, int i) __attribute__((always_inline)) {
     const uint8_t* src = Wb + (int64_t)t * kXwTile;
     uint8_t* base = lds + sl * kXwTile + wid * kXwP * 1024;
-    (void)src;
-    (void)base;
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src + doff[i], base + i * 1024, 16, 0, 0);
-#endif
+    lds_dma16(src + doff[i], base + i * 1024);
   };
   auto dma = [&](int t, int sl) {
 #pragma unroll
@@ -137,13 +134,14 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
 #pragma unroll
     for (int ks = 0; ks < kXwKS; ++ks) xf[ks] = *reinterpret_cast<const xw_bf16x8*>(xr + 16 * ks);
   };
-  auto row_inv = [&]() {
+  // the row's RMS (sqrt(mean x^2) + eps, the row factor's reciprocal)
+  auto row_rms = [&]() {
     if constexpr (RS) {
       float ss = 0.f;
 #pragma unroll
       for (int ks = 0; ks < kXwKS; ++ks) ss = sumsq8(xf[ks], ss);
       ss += __shfl_xor(ss, 32, 64);
-      return 1.0f / (sqrtf(ss) * p.inv_sqrt_k + kRmsEps);
+      return sqrtf(ss) * p.inv_sqrt_k + kRmsEps;
     } else {
       return 1.0f;
     }
@@ -151,18 +149,18 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
 
   xw_f32x16 acc[2][2];       // [buffer][g, u]
   uint32_t po[8], pu[8];     // packed bf16 pairs of the epilogue in flight (pu: STORE's second half)
-  // epilogue part k (registers 2k, 2k + 1) of the step held in buffer b: W tile t, output row mrow, row factor inv
+  // epilogue part k (registers 2k, 2k + 1) of the step held in buffer b: W tile t, output row mrow, row factor inv.
+  // The accumulators start from bias x RMS (RS) or the bias, so acc x inv = A.W^T x inv + bias and the part reads
+  // no LDS: a bias read here was the youngest LDS op at its use, i.e. an lgkmcnt(0) that also drained the W
+  // fragment reads in flight
   auto epi_part = [&](int b, int t, int64_t mrow, float inv, int k) __attribute__((always_inline)) {
-    const int u = 16 * (k >> 2) + 8 * lh + 2 * (k & 3);              // hidden column of register 2k within the tile
-    const xw_f32x2 bg = *reinterpret_cast<const xw_f32x2*>(sbias + kXwBN * t + u);
-    const xw_f32x2 bu = *reinterpret_cast<const xw_f32x2*>(sbias + kXwBN * t + 32 + u);
     if constexpr (EPI == EPI_STORE) {
-      // output columns 64 t + u, + 1 (rows 0-31 of the tile) and 64 t + 32 + u, + 1 (rows 32-63): bias, row factor
+      // output columns 64 t + u, + 1 (rows 0-31 of the tile) and 64 t + 32 + u, + 1 (rows 32-63)
       float y[2], z[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        y[e] = fmaf(acc[b][0][2 * k + e], inv, bg[e]);
-        z[e] = fmaf(acc[b][1][2 * k + e], inv, bu[e]);
+        y[e] = RS ? acc[b][0][2 * k + e] * inv : acc[b][0][2 * k + e];
+        z[e] = RS ? acc[b][1][2 * k + e] * inv : acc[b][1][2 * k + e];
       }
       po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{y[0], y[1]}, xw_bf16x2));
       pu[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{z[0], z[1]}, xw_bf16x2));
@@ -175,8 +173,8 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
       float y[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {   // scalar fp32 (packed f32 VALU beside MFMAs costs more than two plain ops)
-        const float g = fmaf(acc[b][0][2 * k + e], inv, bg[e]);
-        const float v = fmaf(acc[b][1][2 * k + e], inv, bu[e]);
+        const float g = RS ? acc[b][0][2 * k + e] * inv : acc[b][0][2 * k + e];
+        const float v = RS ? acc[b][1][2 * k + e] * inv : acc[b][1][2 * k + e];
         const float z = (EPI == EPI_SWIGLU) ? g : v;               // the sigmoid's argument
         const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
         y[e] = (EPI == EPI_SWIGLU) ? g * sg * v : g * sg;
@@ -202,7 +200,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   if (total > 1) dma(ahead.t0 + ahead.j, 1);
   advance(ahead);                                                 // ahead = step 2
   int s = 0;
-  float inv = 1.f;
+  float inv = 1.f, rms = 1.f;
   int64_t mrow = 0;
   int pt = 0;                                                     // previous step's W tile, row, row factor
   int64_t prow = 0;
@@ -221,22 +219,33 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
       // between the epilogue parts of the ping-pong's VALU phase), its last piece before that step's last epilogue
       // part; younger ops: that part's stores, step s - 1's pieces (tile s + 1) and its stores
       constexpr int kLate = kXwS / 2;
-      const int younger = kLate * (s >= 3) + (s + 1 < total ? kXwP : 0) + kXwS * (s >= 2);
+      const int younger = kLate * (s >= 3) + kXwP + kXwS * (s >= 2);
       if (younger == kLate + kXwP + kXwS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLate + kXwP + kXwS) : "memory");
       else vmcnt_dyn(younger);
     }
     barrier_lds();                                                // ... for every wave; slot (s + 2) % 3 free
     if constexpr (first) {
-      inv = row_inv();
+      rms = row_rms();
+      inv = 1.0f / rms;
       mrow = min(cur.mt * kXwBM + wid * 32 + lr, p.M - 1);
     }
-    const bool dma_next = s + 2 < total && !(DBG & 4);
-    const int t2 = ahead.t0 + ahead.j, sl2 = (s + 2) % kXwR;
+    // every step DMAs a tile (the last two of the workgroup re-fetch their own into the free slot): a conditional DMA
+    // or epilogue part is a branch around an LDS op, and at each such join the compiler's wait counter fell back to
+    // lgkmcnt(0) -- a full drain of the fragment reads -- before the next MFMA
+    constexpr bool dma_next = !(DBG & 4);
+    const int t2 = s + 2 < total ? ahead.t0 + ahead.j : t, sl2 = (s + 2) % kXwR;
     const uint8_t* base = lds + (s % kXwR) * kXwTile;
+    {   // accumulators from the bias: register r of lane half h is hidden unit 16 (r >> 3) + 8 h + (r & 7)
+      const float* bt = sbias + kXwBN * t + 8 * lh;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[b][i][r] = 0.f;
+      for (int i = 0; i < 2; ++i) {
+        const xw_f32x4 b0 = *reinterpret_cast<const xw_f32x4*>(bt + 32 * i), b1 = *reinterpret_cast<const xw_f32x4*>(bt + 32 * i + 4);
+        const xw_f32x4 b2 = *reinterpret_cast<const xw_f32x4*>(bt + 32 * i + 16), b3 = *reinterpret_cast<const xw_f32x4*>(bt + 32 * i + 20);
+        acc[b][i] = xw_f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                              b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+        if constexpr (RS) acc[b][i] *= rms;
+      }
+    }
     // W fragments two K-steps ahead of the MFMAs that use them (three register sets)
     xw_bf16x8 wf[3][2];
     auto rdw = [&](int ks, xw_bf16x8(&w)[2]) __attribute__((always_inline)) {
@@ -251,7 +260,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
         w[1] = *reinterpret_cast<const xw_bf16x8*>(a + 32 * kXwRowB);
       }
     };
-    const bool epi = s > 0 && !(DBG & 1);
+    const bool epi = (!first || s > 0) && !(DBG & 1);   // compile-time true past a run's first step
     // K-steps k0 .. k1 - 1, fragments read two steps ahead within the range (none live across a VALU phase)
     auto mfmas = [&](int k0, int k1) __attribute__((always_inline)) {
       rdw(k0, wf[k0 % 3]);
@@ -323,6 +332,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   // the last step's epilogue (buffer 1: runs have even lengths)
 #pragma unroll
   for (int k = 0; k < 8; ++k) epi_part(1, pt, prow, pinv, k);
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the re-fetch DMAs landed before the workgroup's LDS is released
 }
 
 // W tiles per work item: among the even divisors of the W tile count (runs of even length), the one minimising
