@@ -138,11 +138,21 @@ __device__ __forceinline__ uint32_t quant4(float a, float b, float c, float d, f
 // inline asm.  After the builtin form the compiler's wait-count pass no longer counts LDS reads: every later
 // ds_read wait became lgkmcnt(0), a full drain of the reads issued ahead (gemm_xw: 54 lgkmcnt(0) with the builtin,
 // counted waits without the DMA).  The asm form is invisible to that pass; the kernels order their DMAs with explicit
-// vmcnt waits and barriers, which is what makes this safe.
+// vmcnt waits and barriers, which is what makes this safe.  lds_dst must be wave-uniform (as for the builtin).
 __device__ __forceinline__ void lds_dma16(const void* src, void* lds_dst) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst;
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+#else
+  (void)src;
+  (void)lds_dst;
+#endif
+}
+// the 4-byte form (global_load_lds_dword: lane l's dword lands at lds_dst + 4 l)
+__device__ __forceinline__ void lds_dma4(const void* src, void* lds_dst) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
 #else
   (void)src;
   (void)lds_dst;

@@ -200,11 +200,7 @@ __global__ void __launch_bounds__(256) attention_rec_kernel(AttnArgs a) {
   for (int in = 0; in < VINS; ++in) {
     const int pc = min(in * 64 + lane, TK * VPC - 1), j = pc / VPC, e = (pc % VPC) * (16 / ES);
     const uint8_t* src = static_cast<const uint8_t*>(a.v) + (((int64_t)b * TK + j) * a.ldv + c0 + e) * ES;
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src, vs[wid] + in * 1024, 16, 0, 0);
-#else
-    (void)src;
-#endif
+    lds_dma16(src, vs[wid] + in * 1024);
   }
   // Q and K rows, three 4-element loads per row
   auto load_row = [&](const void* base, int64_t row, float (&x)[12]) {

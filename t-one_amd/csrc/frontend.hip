@@ -425,22 +425,13 @@ __global__ void __launch_bounds__(512) conv2_bf16_kernel(const uint16_t* __restr
       const int pc = wid * 2 + h, tap = min(sg * kC2TP + (pc >> 2), kC2Taps);   // past the end: the zero tap
       const int L = (pc & 3) * 64 + lane, c = L >> 2, s = L & 3;
       const uint16_t* src = w2c + (int64_t)c * kConv2KPad + tap * kSub1C + ((s ^ c2_swz(c)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, ring + (sg % 3) * kC2Ring + pc * 256, 16, 0, 0);
-#else
-      (void)src;
-      (void)ring;
-#endif
+      lds_dma16(src, ring + (sg % 3) * kC2Ring + pc * 256);
     }
   };
   for (int pc = wid; pc < kC2SlabPieces; pc += 8) {       // the stream's input, once
     const int L = pc * 64 + lane, q = min(L >> 2, kC2In - 1), s = L & 3;
     const uint16_t* src = xb + q * kSub1C + ((s ^ c2_swz(q)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src, slab + pc * 256, 16, 0, 0);
-#else
-    (void)src;
-#endif
+    lds_dma16(src, slab + pc * 256);
   }
   stage_taps(0);
   stage_taps(1);
@@ -503,12 +494,7 @@ __global__ void __launch_bounds__(512) sub_conv_bf16_kernel(const float* __restr
       const int pc = wid * 2 + h, tap = min(sg * kC2TP + (pc >> 2), kC2Taps);   // past the end: the zero tap
       const int L = (pc & 3) * 64 + lane, c = L >> 2, q = L & 3;
       const uint16_t* src = w2c + (int64_t)c * kConv2KPad + tap * kSub1C + ((q ^ c2_swz(c)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, ring + (sg % 3) * kC2Ring + pc * 256, 16, 0, 0);
-#else
-      (void)src;
-      (void)ring;
-#endif
+      lds_dma16(src, ring + (sg % 3) * kC2Ring + pc * 256);
     }
   };
   stage_taps(0);
@@ -750,11 +736,7 @@ __global__ void __launch_bounds__(512) conv2_p3_kernel(const float* __restrict__
     for (int i = 0; i < 3; ++i) {
       const int pc = wid * 3 + i;
       const uint16_t* src = w2p + (int64_t)j * kP3Tap + pc * 512 + lane * 8;
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, ring + (j % 3) * kP3Tap + pc * 512, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, ring + (j % 3) * kP3Tap + pc * 512);
     }
   };
   // waves 4-7: the fp32 input rows 3 r + kt (r < 5, row past the stream clamped) into the staging area
@@ -766,11 +748,7 @@ __global__ void __launch_bounds__(512) conv2_p3_kernel(const float* __restrict__
       const int rr = e / (kSub1F * kSub1C), o = e - rr * (kSub1F * kSub1C);
       const int row = min(kSub2Stride * (part * kP3Rows + rr) + kt, kIn - 1);
       const float* src = xb + (int64_t)row * kSub1F * kSub1C + o;
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, stg + pc * 256, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, stg + pc * 256);
     }
   };
   // all waves: staging -> the three planes of buffer `buf` (each thread a few 4-channel groups)

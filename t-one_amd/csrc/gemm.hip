@@ -620,17 +620,11 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
       } else {
         src = A + aoff[i] + k0;
       }
-#if defined(__HIP_DEVICE_COMPILE__)   // amdgcn-only builtin; the host pass only sees the kernel's signature
-      __builtin_amdgcn_global_load_lds(src, base + (8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, base + (8 * (wid + i * kNWaves)) * BK);
     }
 #pragma unroll
     for (int i = 0; i < W_I; ++i) {
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(W + woff[i] + k0, base + (BM + 8 * (wid + i * kNWaves)) * BK, 16, 0, 0);
-#endif
+      lds_dma16(W + woff[i] + k0, base + (BM + 8 * (wid + i * kNWaves)) * BK);
     }
   };
 

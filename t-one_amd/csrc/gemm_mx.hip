@@ -172,12 +172,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
       const int c = (lane & 7) ^ mx_swz(row);
       const uint8_t* src = (j < NQW) ? p.W + (int64_t)(n0 + 128 * j + row) * p.K + k0 + 16 * c
                                      : p.A + (int64_t)min(m0 + 128 * (j - NQW) + row, p.M - 1) * p.lda + k0 + 16 * c;
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, dst + piece * 8 * BK, 16, 0, 0);
-#else
-      (void)src;
-      (void)dst;
-#endif
+      lds_dma16(src, dst + piece * 8 * BK);
     }
   };
   auto issue_kt = [&](int u, const Pos& s, int from, int to) {   // quarters [from, to) of K-step u (NQW + XQ each)
@@ -588,11 +583,7 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
 #pragma unroll
     for (int i = 0; i < kX8Pieces; ++i) {
       const uint8_t* src = wt + doff[i];
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + (wid * kX8Pieces + i) * 1024, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, base + (wid * kX8Pieces + i) * 1024);
     }
   };
 

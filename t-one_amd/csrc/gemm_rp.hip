@@ -168,13 +168,7 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
       uint8_t* base = lds + slot * Cfg::kStage;
 #pragma unroll
       for (int j = 0; j < PMAX; ++j) {
-        if (j < np) {
-#if defined(__HIP_DEVICE_COMPILE__)
-          __builtin_amdgcn_global_load_lds(src[j] + kt * 32, base + (wid + 8 * j) * 1024, 16, 0, 0);
-#else
-          (void)base;
-#endif
-        }
+        if (j < np) lds_dma16(src[j] + kt * 32, base + (wid + 8 * j) * 1024);
       }
     };
 
@@ -224,28 +218,16 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
           [[maybe_unused]] const int q = wid + 8 * j;
           if (q < QA + QW) {
             const int r = 8 * (q < QA ? q : q - QA) + (ln >> 3), c = (ln & 7) ^ ((r >> 1) & 7);
-#if defined(__HIP_DEVICE_COMPILE__)
             if (q < QA)
-              __builtin_amdgcn_global_load_lds(A8 + (uint32_t)(min(m0 + r, p.M - 1) * p.lda + 128 * kt + 16 * c),
-                                               base + q * 1024, 16, 0, 0);
+              lds_dma16(A8 + (uint32_t)(min(m0 + r, p.M - 1) * p.lda + 128 * kt + 16 * c), base + q * 1024);
             else
-              __builtin_amdgcn_global_load_lds(W8 + (uint32_t)(r * p.K + 128 * kt + 16 * c), base + BM * 128 + (q - QA) * 1024,
-                                               16, 0, 0);
-#else
-            (void)c;
-#endif
+              lds_dma16(W8 + (uint32_t)(r * p.K + 128 * kt + 16 * c), base + BM * 128 + (q - QA) * 1024);
           } else {
             const int r = 64 * (q < QA + QW + QAS ? q - QA - QW : q - QA - QW - QAS) + ln;
-#if defined(__HIP_DEVICE_COMPILE__)
             if (q < QA + QW + QAS)
-              __builtin_amdgcn_global_load_lds(p.As + (uint32_t)(min(m0 + r, p.M - 1) * p.ldas + 4 * kt),
-                                               base + Cfg::kMxScA + (q - QA - QW) * 256, 4, 0, 0);
+              lds_dma4(p.As + (uint32_t)(min(m0 + r, p.M - 1) * p.ldas + 4 * kt), base + Cfg::kMxScA + (q - QA - QW) * 256);
             else
-              __builtin_amdgcn_global_load_lds(p.Ws + (uint32_t)(r * (p.K / 32) + 4 * kt),
-                                               base + Cfg::kMxScW + (q - QA - QW - QAS) * 256, 4, 0, 0);
-#else
-            (void)r;
-#endif
+              lds_dma4(p.Ws + (uint32_t)(r * (p.K / 32) + 4 * kt), base + Cfg::kMxScW + (q - QA - QW - QAS) * 256);
           }
         }
       };

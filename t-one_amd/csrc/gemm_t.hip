@@ -78,22 +78,14 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_t_kernel(GemmArgs p
     for (int i = 0; i < WP; ++i) {
       const int piece = wid + i * NW, row = piece * 8 + (lane >> 3);
       const uint16_t* src = W + (int64_t)(n0 + row) * p.K + k0 + (((lane & 7) ^ ((row >> 1) & 7)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + piece * 8 * BK, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, base + piece * 8 * BK);
     }
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int piece = wid + i * NW, row = piece * 8 + (lane >> 3);
       const int gm = min(m0 + row, p.M - 1);
       const uint16_t* src = X + (int64_t)gm * p.lda + k0 + (((lane & 7) ^ ((row >> 1) & 7)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + (BNW + piece * 8) * BK, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, base + (BNW + piece * 8) * BK);
     }
   };
 
@@ -218,22 +210,14 @@ __global__ void __launch_bounds__(256) gemm_t2_kernel(GemmArgs p) {
     for (int i = 0; i < WP; ++i) {
       const int piece = wid + i * NW, row = piece * 16 + (lane >> 2);
       const uint16_t* src = W + (int64_t)(n0 + row) * p.K + k0 + (((lane & 3) ^ ((row >> 2) & 3)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + piece * 16 * BK, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, base + piece * 16 * BK);
     }
 #pragma unroll
     for (int i = 0; i < XP; ++i) {
       const int piece = wid + i * NW, row = piece * 16 + (lane >> 2);
       const int gm = min(m0 + row, p.M - 1);
       const uint16_t* src = X + (int64_t)gm * p.lda + k0 + (((lane & 3) ^ ((row >> 2) & 3)) << 3);
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + (BNW + piece * 16) * BK, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, base + (BNW + piece * 16) * BK);
     }
   };
 
@@ -355,11 +339,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_f32t_kerne
       const int k0 = (kt * WK + g) * EPR + ((lane & 7) ^ ((row >> 1) & 7)) * EPS;
       const E* src = row < BNW ? W + (int64_t)(n0 + row) * p.K + k0
                                : X + (int64_t)min(m0 + row - BNW, p.M - 1) * p.lda + k0;
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + g * GROUP + pr * 8 * 32, 16, 0, 0);
-#else
-      (void)src;
-#endif
+      lds_dma16(src, base + g * GROUP + pr * 8 * 32);
     }
   };
 
@@ -577,12 +557,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
         src = X + (int64_t)min(m0 + row, p.M - 1) * p.lda + kb + slot * 4;
         dst = base + g * GROUP + 3 * WPL + rb * 32;
       }
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-#else
-      (void)src;
-      (void)dst;
-#endif
+      lds_dma16(src, dst);
     }
   };
 
@@ -864,12 +839,7 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * 64) gemm_r3_kernel(GemmArgs 
       const float* src;
       if (i * NW < BN / 8) src = W + (int64_t)(n0 + r) * p.K + k0 + 4 * c;   // folds after unrolling
       else src = X + (int64_t)min(m0 + r - BN, p.M - 1) * p.lda + k0 + 4 * c;
-#if defined(__HIP_DEVICE_COMPILE__)
-      __builtin_amdgcn_global_load_lds(src, base + pc * 256, 16, 0, 0);
-#else
-      (void)src;
-      (void)base;
-#endif
+      lds_dma16(src, base + pc * 256);
     }
   };
 
