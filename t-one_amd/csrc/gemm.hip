@@ -538,7 +538,11 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_kernel(GemmArgs p) 
 // 128-byte rows of A and W straight into LDS with global_load_lds_dwordx4 (one wave instruction =
 // 8 rows x 128 B), the next K-step's DMA in flight while the MFMAs run on the current buffer.
 // LDS rows are lane-linear, so the ds_read_b128 bank spread comes from an XOR swizzle applied to
-// the per-lane SOURCE address (16-byte slot ^= row & 7) and undone on the read (guide rule 21).
+// the per-lane SOURCE address (16-byte slot ^= (row >> 1) & 7) and undone on the read (guide rule 21).  Two
+// 128-byte rows share a 256-byte bank window, so a 16-lane ds_read_b128 group (rows {0-3, 12-15, 20-27} or
+// {4-11, 16-19, 28-31} of the 32-row fragment) needs 8 distinct slots per row parity: (row >> 1) & 7 gives them;
+// round 4's row & 7 repeated each slot twice (41-48 % of the kernel's LDS cycles were conflict cycles,
+// profiles/r05_pmc_lds_bf16.txt).
 // A rowscale GEMM reads the bf16 shadow of the residual and takes each row's sum of squares from
 // its own A fragments (waves of the first N column only).
 // Split-K is a runtime mode here (p.k_split > 0: K slice blockIdx.y, raw partials to p.ws).
@@ -589,7 +593,7 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
   for (int i = 0; i < A_I; ++i) {
     const int row = 8 * (wid + i * kNWaves) + lrow8;
     const int gm = min(m0 + row, p.M - 1);
-    aslot[i] = lslot ^ (row & 7);
+    aslot[i] = lslot ^ ((row >> 1) & 7);
     if constexpr (CONV2) {
       const int b = gm / (p.conv_t * kSub2F), rem = gm % (p.conv_t * kSub2F);
       const int t = rem / kSub2F, f = rem % kSub2F;
@@ -603,7 +607,7 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
 #pragma unroll
   for (int i = 0; i < W_I; ++i) {
     const int row = 8 * (wid + i * kNWaves) + lrow8;
-    woff[i] = (int64_t)(n0 + row) * p.K + (lslot ^ (row & 7)) * 8;
+    woff[i] = (int64_t)(n0 + row) * p.K + (lslot ^ ((row >> 1) & 7)) * 8;
   }
 
   auto stage = [&](int buf, int k0) {
@@ -669,12 +673,12 @@ __global__ void __launch_bounds__(TL::WM * TL::WN * 64) gemm_glds_kernel(GemmArg
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WTM + i * 32 + lr;
-        a[ks][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((slot ^ (row & 7)) << 3));
+        a[ks][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((slot ^ ((row >> 1) & 7)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WTN + j * 32 + lr;
-        b[ks][j] = *reinterpret_cast<const bf16x8*>(base + (BM + row) * BK + ((slot ^ (row & 7)) << 3));
+        b[ks][j] = *reinterpret_cast<const bf16x8*>(base + (BM + row) * BK + ((slot ^ ((row >> 1) & 7)) << 3));
       }
     }
 #pragma unroll
