@@ -6,9 +6,9 @@ set -u
 mkdir -p gpurun_out
 out=gpurun_out/r05_xw_ablate2.jsonl
 : > $out
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for M in 40960 20480; do
-    for dbg in 0 1 2 3 4 16 19 64 192; do
+    for dbg in ${DBGS:-0 1 2 3 4 16 19 64 192}; do
       ROWSCALE=1 XSDBG=$dbg timeout -k 10 60 ./t-one_amd/gemm_bench_ablate $M 384 3072 2 -300 1 20 | sed "s/}\$/, \"dbg\": $dbg}/" >> $out || exit $?
     done
   done

@@ -60,7 +60,8 @@ struct XwPos {
   int item, j, n, t0, mt;
 };
 
-// DBG (XW_ABLATE microbenchmark builds only; 1-16 are timing only, the results are wrong): 1 no epilogue (the MFMAs
+// DBG (XW_ABLATE microbenchmark builds only; 1-16 and 256 are timing only, the results are wrong): 256 no output stores,
+// 1 no epilogue (the MFMAs
 // and fragment reads are then dead code too), 2 no MFMA, 4 no W DMA after the prologue, 16 no W fragment reads, 64 a
 // ping-pong schedule instead of the interleaved one (waves 0-3: half the K-steps, the whole VALU phase, the other
 // half; waves 4-7: VALU phase first), 128 (with 64) the waves 0-3 order for all waves.  Measured at M = 40960
@@ -182,7 +183,8 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
       po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{y[0], y[1]}, xw_bf16x2));
       if ((k & 3) == 3) {   // registers 0-7 / 8-15 done: 8 consecutive hidden columns, one 16-byte store
         const xw_u32x4 w = {po[k - 3], po[k - 2], po[k - 1], po[k]};
-        *reinterpret_cast<xw_u32x4*>(Cout + mrow * p.ldc + 32 * t + 16 * (k >> 2) + 8 * lh) = w;
+        if constexpr ((DBG & 256) != 0) asm volatile("" ::"v"(w));   // no stores (timing only)
+        else *reinterpret_cast<xw_u32x4*>(Cout + mrow * p.ldc + 32 * t + 16 * (k >> 2) + 8 * lh) = w;
       }
     }
   };
@@ -359,7 +361,7 @@ hipError_t launch_xw(const GemmArgs& a, int nc, hipStream_t st) {
   if constexpr (EPI == EPI_SWIGLU) {
     switch (a.rowscale ? a.dbg : 0) {
 #define XW_D(d) case d: hipLaunchKernelGGL((gemm_xw_kernel<EPI, true, d>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc); return hipGetLastError();
-      XW_D(1) XW_D(2) XW_D(3) XW_D(4) XW_D(16) XW_D(19) XW_D(64) XW_D(192)
+      XW_D(1) XW_D(2) XW_D(3) XW_D(4) XW_D(16) XW_D(19) XW_D(64) XW_D(192) XW_D(256) XW_D(258)
 #undef XW_D
       default: break;
     }
