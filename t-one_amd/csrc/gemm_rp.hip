@@ -353,6 +353,12 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
       continue;
     }
 
+    // MX: the last K-tile's fragments are read from stage slot (nk - 1) & 1 during that step, and the image, bias and
+    // gain below sit on slot 0: with an odd K-tile count (K = 384: 3) a wave that finished its MFMAs early overwrote
+    // fragments another wave was still reading (gemm_bench RPMX at M = 20480, K = 384: max rel error 0.76).  The
+    // bf16 ring's last step reads only a spent slot ahead, so it needs no barrier here.
+    if constexpr (MX) barrier_lds();
+
     // epilogue, one 16-row sweep at a time (its accumulators die as it goes): the wave row that owns sweep s writes
     // tile row s % FM to an LDS image slot (two slots alternate, one barrier per sweep), then every lane takes 3
     // 16-byte vectors of one row
