@@ -77,3 +77,36 @@ def test_xs8_swiglu_matches_reference(M):
     _gpu()
     r = _run(M, 384, 3072, 2, 98, {"ROWSCALE": 1})
     assert r["max_rel_err"] < 0.3, r
+
+
+# the fp32 step's GEMMs through gemm()'s own routing (gemm_x3 tiles, its 3-way split K at 400 ms, gemm_r3, gemm_sm at
+# M <= 64), full fp32 operands against the fp64 reference: (K, N, epi, row factor) of FFN up, FFN down, attn-out / pw2,
+# pw1 and q|k|v, at B = 256 (T = 10 / 5), 400 ms (T = 13 / 6) and the drop-in's B = 1 / 6
+FP32_OPS = [(384, 3072, 2, 1), (1536, 384, 1, 0), (384, 384, 1, 0), (384, 768, 3, 1), (384, 1152, 0, 1)]
+
+
+@pytest.mark.parametrize("M", [2560, 1280, 3328, 1536, 60, 10])
+@pytest.mark.parametrize("K,N,epi,rs", FP32_OPS)
+def test_fp32_routes_match_reference(M, K, N, epi, rs):
+    _gpu()
+    r = _run(M, K, N, epi, -2, {"FULLF32": 1, "NOC2": 1, "ROWSCALE": rs})
+    assert r["max_rel_err"] < 2e-5, r
+
+
+# the bf16 step's GEMMs through gemm()'s routing below the large-batch kernels (gemm_glds, gemm_t; B = 512 .. 1638)
+@pytest.mark.parametrize("M", [10240, 5120, 2560])
+@pytest.mark.parametrize("K,N,epi,rs", FP32_OPS)
+def test_bf16_routes_match_reference(M, K, N, epi, rs):
+    _gpu()
+    r = _run(M, K, N, epi, -1, {"RES16": int(epi == 1), "ROWSCALE": rs})   # the fp16 residual on RESID only
+    assert r["max_rel_err"] < 1e-2, r
+
+
+# fp8 mode below the row-panel / X-stationary routes: the persistent MXFP8 kernel (gemm_mx) for q|k|v (fp32 out),
+# FFN down (fp16 residual) and FFN up (SwiGLU -> MXFP8 h: its rounding, as for gemm_xs8)
+@pytest.mark.parametrize("M", [10240, 5120, 2560])
+@pytest.mark.parametrize("K,N,epi,rs,tol", [(384, 1152, 0, 1, 2e-3), (1536, 384, 1, 0, 2e-3), (384, 3072, 2, 1, 0.3)])
+def test_mx_routes_match_reference(M, K, N, epi, rs, tol):
+    _gpu()
+    r = _run(M, K, N, epi, 99, {"RES16": int(epi == 1), "ROWSCALE": rs})
+    assert r["max_rel_err"] < tol, r
