@@ -307,14 +307,16 @@ def test_bf16_mode_close_to_oracle(weights, oracle):
     s.close()
 
 
-def test_bf16_pre_encode_stage(weights, oracle):
-    """bf16 front end + subsampling (sub1 Toeplitz MFMA, conv2 LDS-slab kernel, Linear, out_norm) vs the
-    oracle's pre-encode output from a carried state: relative L2 error at bf16 level."""
+@pytest.mark.parametrize("b", [3, 64])
+def test_bf16_pre_encode_stage(weights, oracle, b):
+    """bf16 front end + subsampling (sub_conv_bf16: conv1 + conv2 from one LDS slab, Linear, out_norm) vs the
+    oracle's pre-encode output from a carried state: relative L2 error at bf16 level, and per frame the largest
+    element error against that frame's largest value (a race or a wrong tile shows as O(1) there).  Measured on
+    MI355X (scripts/probe_preencode.py, profiles/r05_probe_preencode.txt): relative L2 0.0042, worst frame 0.0062."""
     _gpu()
     from tone_amd.model import ToneSession
-    s = ToneSession(weights, precision="bf16", max_batch=4)
+    s = ToneSession(weights, precision="bf16", max_batch=b)
     rng = np.random.default_rng(23)
-    b = 3
     _, st0 = oracle.step(synthetic_pcm(rng, b, 0.0), None)
     pcm = synthetic_pcm(rng, b, 0.0)
     trace = []
@@ -328,7 +330,8 @@ def test_bf16_pre_encode_stage(weights, oracle):
         s.close()
     ref = trace[1]
     rel = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
-    assert rel < 2e-2, rel
+    frame = float((np.abs(got - ref).max(-1) / np.abs(ref).max(-1)).max())
+    assert rel < 1e-2 and frame < 2e-2, (rel, frame)
 
 
 @pytest.mark.parametrize("prec,b,n", [("bf16", 512, 10), ("bf16", 2048, 10), ("bf16", 4096, 10), ("fp8", 4096, 10)])
