@@ -702,3 +702,41 @@ def test_nan_propagates(weights, prec):
     finally:
         s.close()
     assert np.isnan(lp).all(), f"{prec}: {np.isnan(lp).mean():.3f} of the logprobs are NaN"
+
+
+@pytest.mark.parametrize("prec,b,bound", [("bf16", 4096, 0.03), ("fp8", 4096, 0.15), ("bf16", 2048, 0.03)])
+def test_lowprec_stagewise_large_batch(weights, oracle, prec, b, bound):
+    """bf16 / fp8 at the bench's batches (the large-batch routes: gemm_xw / gemm_xs8, gemm_rp / gemm_rp_mx, dwconv,
+    sub_conv, the recomputing attention), stage by stage against the oracle on 8 sampled streams from a carried state:
+    per (stream, frame) row the largest element error over the row's largest value.  Measured on MI355X
+    (scripts/probe_stagewise_lowprec.py, profiles/r05_probe_stagewise_lowprec.txt): bf16 <= 0.008 at every stage, fp8
+    <= 0.058 (growing through the layers); the bounds are ~4x / ~2.5x that -- far tighter than the step tests'
+    logprob bounds (fp8 max 0.6).  (The gemm_rp_mx race that test_gpu_kernels.py catches did not show on these
+    sampled rows in the step: the build before its fix passes this test too, profiles/r05_stagewise_prev.log.)"""
+    _gpu()
+    import torch
+    from tone_amd.model import ToneSession
+    s = ToneSession(weights, precision=prec, max_batch=b)
+    rng = np.random.default_rng(31)
+    pick = np.sort(rng.choice(b, 8, replace=False))
+    pcm0 = synthetic_pcm(rng, b, 0.0)
+    pcm1 = synthetic_pcm(rng, b, 0.0)
+    worst = []
+    try:
+        st = torch.zeros((b, C.STATE_SIZE), dtype=torch.float16, device=s.dev)
+        _, st = s.step(torch.from_numpy(pcm0).to(s.dev), st)
+        trace = []
+        oracle.step(pcm1[pick], st.cpu().numpy()[pick], trace=trace)
+        for stage, ref in enumerate(trace):
+            if stage == 0:
+                continue
+            s.debug_stop(stage)
+            s.step(torch.from_numpy(pcm1).to(s.dev), st.clone())
+            layer = stage - 2
+            reduced = C.REDUCTION_POS <= layer < C.UPSAMPLE_POS
+            got = s.debug_read("rB" if reduced else "rA", (b, 5 if reduced else 10, C.D_MODEL))[pick]
+            worst.append(float((np.abs(got - ref).max(-1) / np.abs(ref).max(-1)).max()))
+    finally:
+        s.debug_stop(-1)
+        s.close()
+    assert max(worst) < bound, " ".join(f"{i + 1}:{v:.3f}" for i, v in enumerate(worst))
