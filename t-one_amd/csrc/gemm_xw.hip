@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   // The accumulators start from bias x RMS (RS) or the bias, so acc x inv = A.W^T x inv + bias and the part reads
   // no LDS: a bias read here was the youngest LDS op at its use, i.e. an lgkmcnt(0) that also drained the W
   // fragment reads in flight
-  auto epi_part = [&](int b, int t, int64_t mrow, float inv, int k) __attribute__((always_inline)) {
+  auto epi_part = [&](int b, int t, int64_t mrow, float inv, float cz, float inv2, int k) __attribute__((always_inline)) {
     if constexpr (EPI == EPI_STORE) {
       // output columns 64 t + u, + 1 (rows 0-31 of the tile) and 64 t + 32 + u, + 1 (rows 32-63)
       float y[2], z[2];
@@ -174,11 +174,13 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
       float y[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {   // scalar fp32 (packed f32 VALU beside MFMAs costs more than two plain ops)
-        const float g = RS ? acc[b][0][2 * k + e] * inv : acc[b][0][2 * k + e];
-        const float v = RS ? acc[b][1][2 * k + e] * inv : acc[b][1][2 * k + e];
-        const float z = (EPI == EPI_SWIGLU) ? g : v;               // the sigmoid's argument
-        const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z * -1.4426950408889634f));
-        y[e] = (EPI == EPI_SWIGLU) ? g * sg * v : g * sg;
+        // the row factor rides on the sigmoid's exp2 scale (cz = inv * -log2 e) and, for SwiGLU, on the product once
+        // (inv2 = inv^2): g * sigmoid(g) * v = (acc_g acc_u inv^2) / (1 + exp2(acc_g cz)), one multiply per output
+        // fewer than scaling g and v first
+        const float ag = acc[b][0][2 * k + e], au = acc[b][1][2 * k + e];
+        const float za = (EPI == EPI_SWIGLU ? ag : au) * (RS ? cz : -1.4426950408889634f);
+        const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(za));
+        y[e] = (EPI == EPI_SWIGLU) ? (RS ? (ag * au) * inv2 : ag * au) * sg : (RS ? ag * inv : ag) * sg;
       }
       po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(xw_f32x2{y[0], y[1]}, xw_bf16x2));
       if ((k & 3) == 3) {   // registers 0-7 / 8-15 done: 8 consecutive hidden columns, one 16-byte store
@@ -206,7 +208,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   int64_t mrow = 0;
   int pt = 0;                                                     // previous step's W tile, row, row factor
   int64_t prow = 0;
-  float pinv = 1.f;
+  float pinv = 1.f, pcz = -1.4426950408889634f, pinv2 = 1.f;   // previous step's row factor, inv * -log2 e, inv^2
 
   auto step = [&](auto Bc, auto Fc, auto Lc) __attribute__((always_inline)) {
     constexpr int b = decltype(Bc)::value;
@@ -279,7 +281,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
         }
         if constexpr ((DBG & 64) == 0) {   // interleaved schedule: DMA piece / epilogue part between the MFMAs
           if (dma_next && ks % 4 == 2) dma_piece(t2, sl2, ks / 4);
-          if (epi && ks % 3 == 1) epi_part(b ^ 1, pt, prow, pinv, ks / 3);
+          if (epi && ks % 3 == 1) epi_part(b ^ 1, pt, prow, pinv, pcz, pinv2, ks / 3);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -288,7 +290,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
     auto valu_phase = [&]() __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        if (epi) epi_part(b ^ 1, pt, prow, pinv, k);
+        if (epi) epi_part(b ^ 1, pt, prow, pinv, pcz, pinv2, k);
         if (k < kXwP && dma_next) dma_piece(t2, sl2, k);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -311,6 +313,8 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
     pt = t;
     prow = mrow;
     pinv = inv;
+    pcz = inv * -1.4426950408889634f;
+    pinv2 = inv * inv;
     advance(cur);
     advance(ahead);
     ++s;
@@ -333,7 +337,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   }
   // the last step's epilogue (buffer 1: runs have even lengths)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) epi_part(1, pt, prow, pinv, k);
+  for (int k = 0; k < 8; ++k) epi_part(1, pt, prow, pinv, pcz, pinv2, k);
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the re-fetch DMAs landed before the workgroup's LDS is released
 }
 
