@@ -462,6 +462,27 @@ def spawn_ranks(n: int, argv: list[str], timeout_s: float | None = None, script:
                               stdout=None if r == 0 else subprocess.DEVNULL)
              for r, e in enumerate(rank_envs(n, port))]
     t_end = None if timeout_s is None else time.monotonic() + timeout_s
+
+    def stop_ranks(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    # the ranks run in their own sessions: if this parent is terminated or interrupted (a driver's own timeout,
+    # Ctrl-C), take them down with it instead of leaving them holding the GPUs
+    def on_signal(signum, _frame):
+        stop_ranks(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                stop_ranks(signal.SIGKILL)
+        os._exit(128 + signum)
+
+    prev = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)}
     status = 0
     while True:
         codes = [p.poll() for p in procs]
@@ -472,17 +493,17 @@ def spawn_ranks(n: int, argv: list[str], timeout_s: float | None = None, script:
             break
         if bad or (t_end is not None and time.monotonic() > t_end):
             status = status or 124
-            for p in procs:
-                if p.poll() is None:
-                    os.killpg(p.pid, signal.SIGTERM)
+            stop_ranks(signal.SIGTERM)
             for p in procs:
                 try:
                     p.wait(timeout=20)
                 except subprocess.TimeoutExpired:
-                    os.killpg(p.pid, signal.SIGKILL)
+                    stop_ranks(signal.SIGKILL)
                     p.wait()
             break
         time.sleep(0.2)
+    for sg, h in prev.items():
+        signal.signal(sg, h)
     if status < 0:
         status = 128 - status          # killed by a signal
     if status:

@@ -649,7 +649,9 @@ __global__ void __launch_bounds__(512) sub_conv_bf16_kernel(const float* __restr
       c1_epi(t1, accB);
     }
   }
+#ifndef SUBCONV_DROP_BARRIER   // test-only build (Makefile kernel_check_nobar): shows tests/test_gpu_kernels.py sees the race
   __syncthreads();                                        // the slab is complete; ring slots 1-2 are free
+#endif
   stage_taps(1);
   conv2_taps(lds, sc, sh, stage_taps, flat, b, wid, lane);
 }

@@ -894,7 +894,8 @@ static hipError_t gemm_bf16(const GemmArgs& a, int epi, hipStream_t st, bool* c8
   *c8_done = false;
   // large batches: the persistent transposed-orientation kernels (gemm_t.hip, tools/gemm_bench sweep)
   // the residual-output projections (N = 384) at large M: whole rows per workgroup (gemm_rp.hip)
-  if (epi == EPI_RESID && a.res16 && a.N == 384 && gemm_rp_routed(a.M, a.K)) {
+  // (an argument set it does not implement falls through to the tiled kernels)
+  if (epi == EPI_RESID && gemm_rp_routed(a.M, a.K) && gemm_rp_accepts(a)) {
     *c8_done = true;
     return gemm_rp(a, st);
   }
@@ -996,7 +997,7 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   if (a.att.probs) return (!bf16 && epi == EPI_RESID && a.M <= 64) ? gemm_sm(a, epi, st) : hipErrorInvalidValue;
   // a fused row norm exists on the row-panel kernel only
   if (a.norm_w)
-    return (bf16 && a.a_bf16 && epi == EPI_RESID && a.res16 && gemm_rp_routed(a.M, a.K)) ? gemm_rp(a, st)
+    return (bf16 && epi == EPI_RESID && gemm_rp_routed(a.M, a.K) && gemm_rp_accepts(a)) ? gemm_rp(a, st)
                                                                                        : hipErrorInvalidValue;
   // the fp16 residual stream exists in the bf16 / fp8 modes only (the LDS-DMA and f32t kernels of gemm_bf16)
   if (a.res16 && (!bf16 || !a.a_bf16 || a.c_bf16 || (epi != EPI_STORE && epi != EPI_RESID))) return hipErrorInvalidValue;

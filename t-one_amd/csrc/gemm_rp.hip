@@ -400,7 +400,11 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) ss += v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
         ss = rp_sum32(ss);
-        const float inv = __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss) * 0.05103103630798288f + kRmsEps);   // 384^-0.5
+        // IEEE sqrt and one IEEE reciprocal of (rms + eps) per row, then a multiply per element: rmsnorm_kernel
+        // (encoder.hip) divides each element and adds the squares in another order, so the two forms differ in the last
+        // bit (a true division per element here cost 5-7 us per launch: 63.7 -> 70.8 us at M = 40960, K = 1536,
+        // profiles/r06_kt1_rp_norm_cost.jsonl)
+        const float inv = 1.0f / (sqrtf(ss) * 0.05103103630798288f + kRmsEps);   // 384^-0.5
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const f32x4*>(sgain + 4 * (eq + 32 * i)) * (v[i] * inv);
       }
@@ -487,11 +491,19 @@ bool gemm_rp_routed(int M, int K) {
   return K % 32 == 0 && M >= 16384;
 }
 
-hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm) {
+bool gemm_rp_accepts(const GemmArgs& a) {
+  // what the kernel implements: RESID on bf16 A / W, N = 384, the fp16 residual, no row factor, no grouped A rows, no
+  // split planes and no K split (those fields are not read by it, so an argument set using them is refused)
   if (a.N != kRpN || a.K % 32 || a.K < 32 || a.M <= 0 || !a.a_bf16 || !a.res16 || a.c_bf16 || a.lda % 8 ||
-      a.ldc % 8 || a.ldr % 4 || !a.R)
-    return hipErrorInvalidValue;
-  if (a.C8 && (!a.C2 || !a.C8s || !a.ss8 || a.ldc != a.N)) return hipErrorInvalidValue;
+      a.ldc % 8 || a.ldr % 4 || !a.R || !a.W)
+    return false;
+  if (a.rowscale || a.rpg || a.a_plane || a.c_plane || a.c2_plane || a.k_split || a.W3 || a.dw.w || a.att.probs)
+    return false;
+  return !a.C8 || (a.C2 && a.C8s && a.ss8 && a.ldc == a.N);
+}
+
+hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm) {
+  if (!gemm_rp_accepts(a)) return hipErrorInvalidValue;
   RpArgs r{};
   r.A = a.A; r.lda = a.lda; r.W = a.W; r.bias = a.bias; r.R = a.R; r.ldr = a.ldr; r.C = a.C; r.ldc = a.ldc;
   r.C2 = a.C2; r.C8 = a.C8; r.C8s = a.C8s; r.ss8 = a.ss8; r.norm_w = a.norm_w; r.alpha = a.alpha;

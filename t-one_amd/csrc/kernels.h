@@ -10,10 +10,13 @@
 namespace tone {
 
 // Experiment switches, read from the environment ONCE per process (the first call; A/B runs compare separate
-// processes).  Defaults are the measured best; none of them changes the arithmetic.
+// processes).  Defaults are the measured best; none of them changes the formulas or the rounding points (rp_norm
+// changes the last bit, see there).
 struct Knobs {
-  int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand
-  int rp_norm;         // TONE_RP_NORM=0: norm_out as its own launch instead of inside FFN2 down (gemm_rp)
+  int fp8_normq;       // TONE_FP8_NORMQ=0: separate quant_mx launches instead of the norm-fused MXFP8 operand (bit-identical)
+  int rp_norm;         // TONE_RP_NORM=0: norm_out as its own launch instead of inside FFN2 down (gemm_rp).  NOT
+                       // bit-identical: the fused form adds the row's squares in another order and multiplies by one
+                       // reciprocal per row instead of dividing each element (last-bit differences of the residual)
 };
 const Knobs& knobs();
 
@@ -88,6 +91,8 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
 hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm = 0);
 // whether gemm() routes a bf16-mode RESID projection of M rows and depth K to gemm_rp (so a norm can be fused)
 bool gemm_rp_routed(int M, int K);
+// whether gemm_rp implements this argument set (it refuses row factors, grouped rows, split planes, a K split ...)
+bool gemm_rp_accepts(const GemmArgs& a);
 
 // W tiles per work item of the X-stationary MXFP8 kernel (gemm_xs8: one 256-row X block, one workgroup per
 // CU): the run length minimising rounds x (run + 3), 3 tiles being the per-item cost of loading the X fragments and

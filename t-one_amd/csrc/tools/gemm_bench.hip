@@ -132,15 +132,66 @@ __global__ void ss_to_inv_kernel(const float* ss8, float* inv, int M) {
   if (m < M) inv[m] = mx_row_inv(ss8 + (int64_t)m * kSsSlots);
 }
 
+// the fused block-final RMSNorm of a RESID row (NORMW=1): the residual sum rounded to fp16 as the stream stores it,
+// then w * v / (||v|| / sqrt(N) + 1e-8) in fp64 -- one thread per row, in place over the un-normalized reference
+__global__ void norm_ref_kernel(float* ref, const float* w, int M, int N) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float* r = ref + (int64_t)m * N;
+  double ss = 0.0;
+  for (int n = 0; n < N; ++n) {
+    const double v = (double)__half2float(__float2half_rn(r[n]));
+    ss += v * v;
+  }
+  const double den = sqrt(ss) / sqrt((double)N) + 1e-8;
+  for (int n = 0; n < N; ++n) r[n] = (float)((double)w[n] * ((double)__half2float(__float2half_rn(r[n])) / den));
+}
+
+// Q8=1: the RESID epilogue's MXFP8 form of its bf16 shadow (e4m3 + E8M0) against quant_mx over the same shadow, byte
+// for byte, and the row factor its sum-of-squares slab gives against quant_mx's (relative)
+__global__ void q8_cmp_kernel(const uint8_t* q, const uint8_t* s, const float* ss, const uint8_t* q2, const uint8_t* s2,
+                              const float* ss2, int M, int N, int* bad, float* inv_err) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  int nb = 0;
+  for (int n = 0; n < N; ++n) nb += q[(int64_t)m * N + n] != q2[(int64_t)m * N + n];
+  for (int n = 0; n < N / 32; ++n) nb += s[(int64_t)m * (N / 32) + n] != s2[(int64_t)m * (N / 32) + n];
+  if (nb) atomicAdd(bad, nb);
+  const float a = mx_row_inv(ss + (int64_t)m * kSsSlots), b = mx_row_inv(ss2 + (int64_t)m * kSsSlots);
+  atomicMax(reinterpret_cast<int*>(inv_err), __float_as_int(fabsf(a - b) / fabsf(b)));
+}
+
+struct Q8Bufs {
+  uint8_t *q = nullptr, *s = nullptr, *q2 = nullptr, *s2 = nullptr;
+  float *ss = nullptr, *ss2 = nullptr, *inv_err = nullptr;
+  int* bad = nullptr;
+  void alloc(int M, int N) {
+    CK(hipMalloc(&q, (size_t)M * N)); CK(hipMalloc(&s, (size_t)M * N / 32)); CK(hipMalloc(&ss, (size_t)M * kSsSlots * 4));
+    CK(hipMalloc(&q2, (size_t)M * N)); CK(hipMalloc(&s2, (size_t)M * N / 32)); CK(hipMalloc(&ss2, (size_t)M * kSsSlots * 4));
+    CK(hipMalloc(&bad, 4)); CK(hipMalloc(&inv_err, 4));
+  }
+  // mismatching bytes and the largest relative row-factor difference
+  void check(const uint16_t* C2, int M, int N, int* hbad, float* herr) {
+    CK(launch_quant_mx(C2, N, M, N, q2, s2, ss2, 0));
+    CK(hipMemset(bad, 0, 4)); CK(hipMemset(inv_err, 0, 4));
+    hipLaunchKernelGGL(q8_cmp_kernel, dim3((M + 255) / 256), dim3(256), 0, 0, q, s, ss, q2, s2, ss2, M, N, bad, inv_err);
+    CK(hipMemcpy(hbad, bad, 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(herr, inv_err, 4, hipMemcpyDeviceToHost));
+  }
+};
+
 static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, const float* R, float* ref, float* err,
-                   int M, int N, int K, int epi, int rowscale, int iters, int xs = 0, const __half* R16 = nullptr) {
+                   int M, int N, int K, int epi, int rowscale, int iters, int xs = 0, const __half* R16 = nullptr,
+                   const float* normw = nullptr) {
   // xs: 98 = the X-stationary kernel (gemm_xs8, SWIGLU only; XSNC = W tiles per item, 0 auto)
   const int xsnc = getenv("XSNC") ? atoi(getenv("XSNC")) : 0;
   // RPMX=1 (RESID, with RES16): the row-panel kernel on MXFP8 operands (gemm_rp_mx) instead of gemm_mx
   const int rpmx = getenv("RPMX") ? atoi(getenv("RPMX")) : 0;
   auto mx = [&](const MxArgs& a) {
-    return xs ? gemm_xs8(a, epi, xsnc, 0) : (rpmx && epi == 1) ? gemm_rp_mx(a, nullptr, 0) : gemm_mx(a, epi, 0);
+    return xs ? gemm_xs8(a, epi, xsnc, 0) : (rpmx && epi == 1) ? gemm_rp_mx(a, normw, 0) : gemm_mx(a, epi, 0);
   };
+  // Q8=1 (gemm_rp_mx RESID): also the shadow's MXFP8 form + slab, checked against quant_mx of the shadow
+  const bool q8 = rpmx && epi == 1 && getenv("Q8") && atoi(getenv("Q8"));
   const int nout = epi >= 2 ? N / 2 : N;
   uint8_t *A8, *As, *W8, *Ws, *C8, *C8s;
   float *inv, *ss8, *Af, *Wf, *C, *Cf;
@@ -157,9 +208,11 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   hipLaunchKernelGGL(dequant_mx_kernel, dim3((unsigned)(((int64_t)N * K + 255) / 256)), dim3(256), 0, 0, W8, Ws, Wf, (int64_t)N, K);
   // NOREF=1: no fp64 reference (timing / counter runs: under rocprofv3 --pmc the naive reference takes minutes)
   const bool noref = getenv("NOREF") && atoi(getenv("NOREF"));
-  if (!noref)
+  if (!noref) {
     hipLaunchKernelGGL(ref_mx_kernel, dim3((nout + 255) / 256, M), dim3(256), 0, 0, Af, Wf, bias, R, rowscale ? inv : nullptr,
                        ref, M, N, K, epi);
+    if (normw && rpmx && epi == 1) hipLaunchKernelGGL(norm_ref_kernel, dim3((M + 255) / 256), dim3(256), 0, 0, ref, normw, M, N);
+  }
   // LDAPAD: X rows at a pitch of K + LDAPAD bytes (L2 channel spread of the row-strided K-tile reads)
   const int pad = getenv("LDAPAD") ? atoi(getenv("LDAPAD")) : 0;
   uint8_t* A8p = A8;
@@ -175,6 +228,13 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   a.C8 = C8; a.C8s = C8s; a.ldc8s = nout / 32; a.M = M; a.N = N; a.K = K;
   a.dbg = getenv("MXDBG") ? atoi(getenv("MXDBG")) : 0;   // gemm_mx.hip DBG bits (SWIGLU only)
   if (epi >= 2) a.ldc = nout;   // bytes of C8 rows
+  Q8Bufs qb;
+  uint16_t* C2q = nullptr;
+  if (q8) {
+    qb.alloc(M, N);
+    CK(hipMalloc(&C2q, (size_t)M * N * 2));
+    a.C2 = C2q; a.Q8 = qb.q; a.Q8s = qb.s; a.ss8 = qb.ss;
+  }
   hipError_t rc = mx(a);
   if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", xs ? 98 : 99, hipGetErrorString(rc)); return; }
   CK(hipDeviceSynchronize());
@@ -185,8 +245,10 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   }
   CK(hipMemset(err, 0, 4));
   hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)chk, a.res16 ? 2 : 0, ref, (int64_t)M * nout, err);
-  float herr;
+  float herr, q8_inv_err = 0.f;
+  int q8_bad = -1;
   CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+  if (q8) qb.check(C2q, M, N, &q8_bad, &q8_inv_err);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int i = 0; i < 3; ++i) CK(mx(a));
@@ -203,8 +265,9 @@ static void run_mx(const uint16_t* A, const uint16_t* W, const float* bias, cons
   CK(hipEventSynchronize(e1));
   float qms;
   CK(hipEventElapsedTime(&qms, e0, e1));
-  printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"quant_us\": %.2f}\n",
-         M, K, N, epi, xs ? 98 : 99, us, 2.0 * M * N * (double)K / us * 1e-6, herr, qms * 1e3 / iters);
+  printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"quant_us\": %.2f, \"norm\": %d, \"q8_bad\": %d, \"q8_inv_err\": %.3g}\n",
+         M, K, N, epi, xs ? 98 : 99, us, 2.0 * M * N * (double)K / us * 1e-6, herr, qms * 1e3 / iters,
+         normw && rpmx && epi == 1 ? 1 : 0, q8_bad, q8_inv_err);
   fflush(stdout);
 }
 
@@ -299,8 +362,8 @@ int main(int argc, char** argv) {
   }
   a.rowscale = rowscale;
   a.inv_sqrt_k = 1.0f / sqrtf((float)K);
-  // NORMW=1: RESID with the fused row RMSNorm (gemm_rp only; gain = 1 + small noise). The error check then compares
-  // against the un-normalized reference (timing only)
+  // NORMW=1: RESID with the fused row RMSNorm (gemm_rp / gemm_rp_mx only; gain = 1 + small noise), checked against the
+  // reference row normalized the same way (norm_ref_kernel)
   float* normw = nullptr;
   if (getenv("NORMW") && atoi(getenv("NORMW"))) {
     std::vector<float> g(N);
@@ -308,6 +371,9 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&normw, N * 4));
     CK(hipMemcpy(normw, g.data(), N * 4, hipMemcpyHostToDevice));
   }
+  float* refn = nullptr;
+  if (normw) CK(hipMalloc(&refn, (size_t)M * nout * 4));
+  Q8Bufs q8b;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const double flop = 2.0 * M * N * (double)K;
@@ -315,7 +381,7 @@ int main(int argc, char** argv) {
   for (char* tok = strtok(list, ","); tok; tok = strtok(nullptr, ",")) {
     const int vv = atoi(tok);
     if (vv == 99 || vv == 98) {   // MXFP8 path: quant_mx + gemm_mx (99) / gemm_xs8 (98) vs an fp64 reference
-      run_mx(A, W, bias, R, ref, err, M, N, K, epi, rowscale, iters, vv == 98, res16 ? R16 : nullptr);
+      run_mx(A, W, bias, R, ref, err, M, N, K, epi, rowscale, iters, vv == 98, res16 ? R16 : nullptr, normw);
       continue;
     }
     // v % 100 = variant (20..23: gemm_t tiles); (v / 100) bits: 1 N-partitioned XCD order,
@@ -338,6 +404,20 @@ int main(int argc, char** argv) {
     a.c_bf16 = f32 ? 0 : cbf;
     a.res16 = res16 && !f32;
     a.norm_w = (v >= 90 && v <= 98) ? normw : nullptr;
+    const float* chk_ref = ref;
+    if (a.norm_w && epi == 1) {   // the normalized reference (once per variant: cheap next to the fp32 reference)
+      CK(hipMemcpy(refn, ref, (size_t)M * nout * 4, hipMemcpyDeviceToDevice));
+      hipLaunchKernelGGL(norm_ref_kernel, dim3((M + 255) / 256), dim3(256), 0, 0, refn, normw, M, N);
+      chk_ref = refn;
+    }
+    // Q8=1 (gemm_rp, RESID with the shadow): the shadow's MXFP8 form + slab, checked against quant_mx of the shadow
+    const bool q8 = v >= 90 && v <= 98 && epi == 1 && a.C2 && getenv("Q8") && atoi(getenv("Q8"));
+    if (q8) {
+      if (!q8b.q) q8b.alloc(M, N);
+      a.C8 = q8b.q; a.C8s = q8b.s; a.ss8 = q8b.ss;
+    } else {
+      a.C8 = nullptr; a.C8s = nullptr; a.ss8 = nullptr;
+    }
     auto launch = [&]() {
       return vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
@@ -355,14 +435,16 @@ int main(int argc, char** argv) {
     if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", v, hipGetErrorString(rc)); continue; }
     CK(hipDeviceSynchronize());
     CK(hipMemset(err, 0, 4));
-    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, a.res16 && epi <= 1 ? 2 : a.c_bf16, ref, (int64_t)M * nout, err);
-    float herr, herr2 = 0.f;
+    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, a.res16 && epi <= 1 ? 2 : a.c_bf16, chk_ref, (int64_t)M * nout, err);
+    float herr, herr2 = 0.f, q8_inv_err = 0.f;
+    int q8_bad = -1;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
     if (a.C2) {   // the bf16 shadow must hold the same values (bf16-rounded)
       CK(hipMemset(err, 0, 4));
-      hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)a.C2, 1, ref, (int64_t)M * nout, err);
+      hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)a.C2, 1, chk_ref, (int64_t)M * nout, err);
       CK(hipMemcpy(&herr2, err, 4, hipMemcpyDeviceToHost));
     }
+    if (q8) q8b.check(a.C2, M, N, &q8_bad, &q8_inv_err);
     for (int i = 0; i < 3; ++i) CK(launch());
     CK(hipEventRecord(e0, 0));
     for (int i = 0; i < iters; ++i) CK(launch());
@@ -371,8 +453,8 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
-    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"shadow_err\": %.3g}\n",
-           M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr, herr2);
+    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"shadow_err\": %.3g, \"norm\": %d, \"q8_bad\": %d, \"q8_inv_err\": %.3g}\n",
+           M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr, herr2, a.norm_w && epi == 1 ? 1 : 0, q8_bad, q8_inv_err);
     fflush(stdout);
   }
   return 0;

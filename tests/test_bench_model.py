@@ -110,6 +110,38 @@ def test_spawn_ranks_passes_rank0_and_propagates_failure(tmp_path, capfd):
     assert bench.spawn_ranks(2, [], 2, script=str(hang)) == 124
 
 
+def test_spawn_ranks_parent_signal_stops_ranks(tmp_path):
+    """A parent terminated while its ranks run (a driver's own timeout) takes the rank process groups with it."""
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    hang = tmp_path / "hang.py"
+    hang.write_text("import os, time\nopen(os.environ['PIDDIR'] + '/' + os.environ['RANK'], 'w').write(str(os.getpid()))\n"
+                    "time.sleep(120)\n")
+    parent = tmp_path / "parent.py"
+    parent.write_text(f"import sys\nsys.path.insert(0, {repr(bench.ROOT)})\nimport bench\n"
+                      f"sys.exit(bench.spawn_ranks(2, [], 100, script={repr(str(hang))}))\n")
+    p = subprocess.Popen([sys.executable, str(parent)], env=dict(__import__("os").environ, PIDDIR=str(tmp_path)))
+    t_end = time.monotonic() + 60
+    while not all((tmp_path / r).exists() and (tmp_path / r).read_text() for r in "01"):
+        assert time.monotonic() < t_end and p.poll() is None
+        time.sleep(0.1)
+    pids = [int((tmp_path / r).read_text()) for r in "01"]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    for pid in pids:        # the ranks are gone (reaped by the parent before it exited)
+        t_end = time.monotonic() + 10
+        while True:
+            try:
+                __import__("os").kill(pid, 0)
+            except ProcessLookupError:
+                break
+            assert time.monotonic() < t_end, pid
+            time.sleep(0.1)
+
+
 def test_summary_line_fits_driver_tail():
     """The printed line keeps every leg's value / ms_per_step / roofline fraction and stays well inside the
     driver's ~8 KB stdout tail; the per-family tables go to the detail file."""

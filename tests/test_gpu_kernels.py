@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.environ.get("TONE_GEMM_BENCH", os.path.join(ROOT, "t-one_amd", "gemm_bench"))   # override: A/B of a build
+CHECK = os.environ.get("TONE_KERNEL_CHECK", os.path.join(ROOT, "t-one_amd", "kernel_check"))
 
 
 def _gpu():
@@ -25,8 +26,8 @@ def _gpu():
 
     if not torch.cuda.is_available():
         pytest.skip("needs a ROCm GPU")
-    if not os.path.exists(BENCH):
-        pytest.fail("t-one_amd/gemm_bench is missing: run __graft_entry__.build()")
+    if not os.path.exists(BENCH) or not os.path.exists(CHECK):
+        pytest.fail("t-one_amd/gemm_bench or kernel_check is missing: run __graft_entry__.build()")
 
 
 def _run(M, K, N, epi, variant, env):
@@ -60,6 +61,33 @@ def test_rp_bf16_resid_matches_reference(M, K):
     _gpu()
     r = _run(M, K, 384, 1, 90, {"RES16": 1})
     assert r["max_rel_err"] < 2e-3 and r["shadow_err"] < 1e-2, r
+
+
+# the fused block-final RMSNorm (NORM) and the shadow's MXFP8 form + sum-of-squares slab (Q8) of the row-panel kernels,
+# at the heights the step routes them (M >= 16384): the normalized rows against the reference normalized the same way
+# (norm_ref_kernel: the residual sum rounded to fp16, then w v / (||v|| / sqrt(384) + 1e-8) in fp64), the MXFP8 bytes
+# against quant_mx over the kernel's own shadow, byte for byte, and the slab's row factor against quant_mx's
+RP_FUSED_SHAPES = [(40960, 1536), (40960, 384), (20480, 1536), (20480, 384), (16384, 384)]
+
+
+@pytest.mark.parametrize("M,K", RP_FUSED_SHAPES)
+@pytest.mark.parametrize("norm,q8", [(1, 0), (0, 1), (1, 1)])
+def test_rp_bf16_norm_q8_matches_reference(M, K, norm, q8):
+    _gpu()
+    r = _run(M, K, 384, 1, 90, {"RES16": 1, "NORMW": norm, "Q8": q8})
+    assert r["norm"] == norm and r["max_rel_err"] < 3e-3 and r["shadow_err"] < 1.2e-2, r
+    if q8:
+        assert r["q8_bad"] == 0 and r["q8_inv_err"] < 1e-5, r
+
+
+@pytest.mark.parametrize("M,K", RP_FUSED_SHAPES)
+@pytest.mark.parametrize("norm,q8", [(1, 0), (0, 1), (1, 1)])
+def test_rp_mx_norm_q8_matches_reference(M, K, norm, q8):
+    _gpu()
+    r = _run(M, K, 384, 1, 99, {"RPMX": 1, "RES16": 1, "NORMW": norm, "Q8": q8})
+    assert r["norm"] == norm and r["max_rel_err"] < 3e-3, r
+    if q8:
+        assert r["q8_bad"] == 0 and r["q8_inv_err"] < 1e-5, r
 
 
 @pytest.mark.parametrize("M,N,epi", [(40960, 3072, 2), (20480, 3072, 2), (4096, 3072, 2), (40960, 768, 3)])
@@ -110,3 +138,143 @@ def test_mx_routes_match_reference(M, K, N, epi, rs, tol):
     _gpu()
     r = _run(M, K, N, epi, 99, {"RES16": int(epi == 1), "ROWSCALE": rs})
     assert r["max_rel_err"] < tol, r
+
+
+# ---- the non-GEMM kernels, every element (t-one_amd/kernel_check, tools/kernel_check.hip) ----------------------------
+# One launch per check at the bench's batches (bf16 / fp8 modes: B = 4096 / 2048; fp32: B = 256 and the drop-in's B = 1),
+# every output element against a naive fp64 GPU reference of the reference model's op over the kernel's own operands,
+# and every element of every state row: the read rows unchanged, the written rows' owned sections equal to the
+# reference (fp16 ulps; copies exact), everything else in them still the sentinel.
+
+
+def _check(*args):
+    out = subprocess.run([CHECK, *map(str, args)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rows = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+    assert rows, out.stdout[-2000:]
+    r = rows[-1]
+    assert r["nan"] == 0, r
+    return r
+
+
+def _state_ok(r, ulp=None, err=None):
+    """ulp: largest fp16 ulp distance allowed (0: the sections are exact copies); err: largest |out - ref| / (1 + |ref|)
+    (recomputed values: one fp16 rounding of a value the kernel computes in another order)."""
+    assert r["state_in_changed"] == 0 and r["state_sentinel_bad"] == 0, r
+    if ulp is not None:
+        assert r["state_ulp"] <= ulp, r
+    if err is not None:
+        assert r["state_err"] < err, r
+
+
+@pytest.mark.parametrize("B", [4096, 2048, 512])
+def test_sub_conv_bf16_every_element(B):
+    """bf16 / fp8 pre-encode at 300 ms (sub_conv_bf16: RMSNorm + conv1 + conv2 in one launch, conformer_blocks.py:631-641):
+    the bf16 flat output within its rounding; the new sub1 / sub2 state rows within an fp16 ulp."""
+    _gpu()
+    r = _check("sub_conv", B)
+    assert r["outputs"]["flat"] < 1e-2, r
+    _state_ok(r, err=2e-3)
+
+
+@pytest.mark.parametrize("check,B,tol", [("sub1_f32", 256, 2e-5), ("sub1_f32", 1, 2e-5), ("sub1_f32_400", 256, 2e-5),
+                                         ("sub1_bf16_400", 4096, 1e-2), ("sub1_bf16_400", 2048, 1e-2)])
+def test_sub1_every_element(check, B, tol):
+    """conv1 alone (fp32 mode, and bf16 at 400 ms): the conv2 input x2 (carried rows + conv1) and the new states."""
+    _gpu()
+    r = _check(check, B)
+    assert r["outputs"]["x2"] < tol, r
+    _state_ok(r, err=2e-3)
+
+
+@pytest.mark.parametrize("check,B,tol", [("conv2_f32", 256, 2e-5), ("conv2_f32", 6, 2e-5), ("conv2_f32", 1, 2e-5),
+                                         ("conv2_f32_400", 256, 2e-5), ("conv2_bf16_400", 4096, 1e-2)])
+def test_conv2_every_element(check, B, tol):
+    """conv2 + BN + SiLU: conv2_p3 (fp32 split, B > 8), conv2_sm (exact fp32, B <= 8), the bf16 implicit GEMM (400 ms)."""
+    _gpu()
+    r = _check(check, B)
+    assert r["outputs"]["flat"] < tol, r
+
+
+DW_CASES = [(4096, t, "dwconv_bf16", 1e-2) for t in (10, 5, 13, 6)] + [(2048, 10, "dwconv_bf16", 1e-2)] + \
+           [(256, t, "dwconv", 1e-5) for t in (10, 5, 13, 6)] + [(1, 10, "dwconv", 1e-5)]
+
+
+@pytest.mark.parametrize("B,T,check,tol", DW_CASES)
+def test_dwconv_every_element(B, T, check, tol):
+    """Depthwise conv k31 + state + BN + SiLU (submodules.py:364-402): output, and the new conv state = exact copies."""
+    _gpu()
+    r = _check(check, B, T)
+    assert r["outputs"]["out"] < tol, r
+    _state_ok(r, 0)
+
+
+REC_TS = [(10, 0), (5, 0), (5, 15), (10, 30), (13, 0), (6, 0), (6, 15), (13, 30)]
+
+
+@pytest.mark.parametrize("T,S", REC_TS)
+@pytest.mark.parametrize("check,B,tol", [("attn_rec_bf16", 4096, 1e-2), ("attn_rec", 256, 5e-5)])
+def test_attention_rec_every_element(T, S, check, B, tol):
+    """Recomputing layers (q/k LayerNorm, RoPE, masked softmax, P V; submodules.py:204-271) for every instantiated
+    (T, S); the probabilities the shared layers reuse, where written; no state write."""
+    _gpu()
+    r = _check(check, B, T, S)
+    assert r["outputs"]["ctx"] < tol, r
+    if "probs" in r["outputs"]:
+        assert r["outputs"]["probs"] < 2e-5, r
+    _state_ok(r, 0)
+
+
+@pytest.mark.parametrize("T", [10, 5, 13, 6])
+@pytest.mark.parametrize("check,B,tol", [("attn_shared_bf16", 4096, 1e-2), ("attn_shared", 256, 1e-5)])
+def test_attention_shared_every_element(T, check, B, tol):
+    _gpu()
+    r = _check(check, B, T)
+    assert r["outputs"]["ctx"] < tol, r
+    _state_ok(r, 0)
+
+
+@pytest.mark.parametrize("T,S", [(5, 15), (10, 30), (6, 15), (13, 30)])
+@pytest.mark.parametrize("check,B,tol", [("kv_bf16", 4096, 1e-2), ("kv", 256, 1e-5)])
+def test_kv_assemble_every_element(T, S, check, B, tol):
+    """Layers 14 / 15 input cache (conformer_blocks.py:147-163): xn, kv = [cache ; xn], the new left-padded cache."""
+    _gpu()
+    r = _check(check, B, T, S)
+    assert r["outputs"]["xn"] < tol and r["outputs"]["kv"] < tol, r
+    _state_ok(r, 1)
+
+
+@pytest.mark.parametrize("T", [10, 13])
+@pytest.mark.parametrize("check,B,tol", [("reduce_bf16", 4096, 1e-2), ("reduce", 256, 1e-5)])
+def test_reduce_conv_every_element(T, check, B, tol):
+    _gpu()
+    r = _check(check, B, T)
+    assert r["outputs"]["y"] < tol, r
+    _state_ok(r, 0)
+
+
+@pytest.mark.parametrize("T", [10, 13])
+@pytest.mark.parametrize("check,B,tol", [("upsample_r16", 4096, 2e-3), ("upsample", 256, 1e-6)])
+def test_upsample_add_every_element(T, check, B, tol):
+    _gpu()
+    r = _check(check, B, T)
+    assert r["outputs"]["x"] < tol and r["outputs"]["shadow"] < 1e-2, r
+
+
+@pytest.mark.parametrize("check,rows", [("head_r16", 40960), ("head_r16", 20480), ("head", 2560), ("head", 60),
+                                        ("head", 10)])
+def test_head_every_element(check, rows):
+    """CTC head + log_softmax + the greedy token / speech flag (head_kernel, and head_rows_kernel at <= 64 rows)."""
+    _gpu()
+    r = _check(check, rows)
+    assert r["outputs"]["logprobs"] < 5e-5 and r["outputs"]["frame_info_bad"] == 0, r
+
+
+@pytest.mark.parametrize("check,rows,tol", [("rmsnorm_q8", 40960, 2e-3), ("rmsnorm_r16", 20480, 2e-3),
+                                            ("rmsnorm", 2560, 1e-5)])
+def test_rmsnorm_every_element(check, rows, tol):
+    _gpu()
+    r = _check(check, rows)
+    assert r["outputs"]["x"] < tol and r["outputs"]["shadow"] < 1e-2, r
+    if "q8_bad_bytes" in r["outputs"]:
+        assert r["outputs"]["q8_bad_bytes"] == 0 and r["outputs"]["q8_row_factor"] < 1e-5, r
