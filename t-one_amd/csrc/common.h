@@ -303,6 +303,18 @@ __device__ __forceinline__ void store_shadow(uint16_t* s, int64_t plane, int64_t
   store_bf16(s, i + 2 * plane, t2);
 }
 
+// The bf16 FFN hidden h between the X-stationary up-projection (gemm_xw) and the row-panel down-projection (gemm_rp),
+// "blocked": a [rows][ld] matrix (ld a multiple of 32, rows padded to a multiple of 32) as 32 x 32 tiles of 2 KiB, tile
+// (row / 32, col / 32) at element ((row / 32) (ld / 32) + col / 32) 1024; inside a tile the 8-column chunk c (columns
+// 8c .. 8c + 7) of row r at element (c >> 1) 512 + ((c & 1) 32 + r) 8.  That is the order in which the 32x32x16
+// MFMA's accumulator registers leave gemm_xw (lane l = 32 h + r holds chunks h and 2 + h of token r): each of its
+// store instructions writes 1 KiB contiguous (row-major h: 32-byte row segments 3 KiB apart), and gemm_rp's 1 KiB
+// DMA pieces read four 256-byte runs (row-major: sixteen 64-byte row segments).  h never leaves that pair.
+__host__ __device__ __forceinline__ int64_t hblk_off(int64_t row, int col, int64_t ld) {
+  const int c = (col & 31) >> 3;
+  return ((row >> 5) * (ld >> 5) + (col >> 5)) * 1024 + (c >> 1) * 512 + ((c & 1) * 32 + (row & 31)) * 8 + (col & 7);
+}
+
 // The residual stream: fp32 in fp32 mode, fp16 in the bf16 / fp8 modes (as the reference's exported graph keeps it,
 // tone/scripts/export.py:411).  Element i, and four consecutive elements (16 / 8-byte aligned),
 // with the type fixed at compile time (R16) or chosen per launch (r16, the GEMM epilogues).

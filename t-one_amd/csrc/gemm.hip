@@ -995,6 +995,12 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   // the depthwise conv in the GLU epilogue exists on gemm_sm only (fp32 mode, M <= 64): no other route
   if (a.dw.w) return (!bf16 && epi == EPI_GLU && a.M <= 64) ? gemm_sm(a, epi, st) : hipErrorInvalidValue;
   if (a.att.probs) return (!bf16 && epi == EPI_RESID && a.M <= 64) ? gemm_sm(a, epi, st) : hipErrorInvalidValue;
+  // the blocked FFN hidden (common.h hblk_off) exists between gemm_xw (SwiGLU out) and gemm_rp (RESID in) only
+  if (a.h_blocked) {
+    if (!bf16 || !a.a_bf16) return hipErrorInvalidValue;
+    if (epi == EPI_SWIGLU) return gemm_xw(a, epi, 0, st);
+    return (epi == EPI_RESID && gemm_rp_accepts(a)) ? gemm_rp(a, st) : hipErrorInvalidValue;
+  }
   // a fused row norm exists on the row-panel kernel only
   if (a.norm_w)
     return (bf16 && epi == EPI_RESID && gemm_rp_routed(a.M, a.K) && gemm_rp_accepts(a)) ? gemm_rp(a, st)

@@ -113,11 +113,13 @@ struct RpArgs {
   const float* norm_w;   // NORM: the row RMSNorm's gain
   float alpha;
   int M, K, dbg;
+  int h_blocked;         // bf16: A in the blocked hidden layout (HB)
 };
 
 // NORM: RMSNorm the output row (gain p.norm_w); Q8: fp8 mode, also the MXFP8 form of the shadow + the slab;
-// MX: MXFP8 operands (v_mfma_scale_f32_16x16x128_f8f6f4), else bf16 (v_mfma_f32_16x16x32_bf16)
-template <int WM, int FM, bool NORM, bool Q8, bool MX>
+// MX: MXFP8 operands (v_mfma_scale_f32_16x16x128_f8f6f4), else bf16 (v_mfma_f32_16x16x32_bf16);
+// HB (bf16): A is the FFN hidden in gemm_xw's blocked tiles (common.h hblk_off), one 32 x 32 tile per K-step and row block
+template <int WM, int FM, bool NORM, bool Q8, bool MX, bool HB = false>
 __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
   using Cfg = RpCfg<WM, FM>;
   constexpr int BM = Cfg::BM, RP = Cfg::RP, FN = Cfg::FN, NA = Cfg::NA, NV = Cfg::NV;
@@ -158,7 +160,8 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
       const int r = 16 * q + (lane >> 2);
       if (q < NA) {
         const int m = min(m0 + r, p.M - 1);
-        src[j] = A + (int64_t)m * p.lda + c * 8;
+        if constexpr (HB) src[j] = A + hblk_off(m, c * 8, p.lda);   // + 1024 per K-step (the next 32 columns' tile)
+        else src[j] = A + (int64_t)m * p.lda + c * 8;
       } else {
         src[j] = W + (int64_t)(r - BM) * p.K + c * 8;
       }
@@ -168,7 +171,8 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
       uint8_t* base = lds + slot * Cfg::kStage;
 #pragma unroll
       for (int j = 0; j < PMAX; ++j) {
-        if (j < np) lds_dma16(src[j] + kt * 32, base + (wid + 8 * j) * 1024);
+        const int ks = (HB && wid + 8 * j < NA) ? 1024 : 32;   // A pieces of a blocked hidden step a whole tile
+        if (j < np) lds_dma16(src[j] + kt * ks, base + (wid + 8 * j) * 1024);
       }
     };
 
@@ -448,6 +452,14 @@ hipError_t launch_rp(const RpArgs& a, hipStream_t st) {
   const int npan = (a.M + Cfg::BM - 1) / Cfg::BM;
   const dim3 grid(npan < 256 ? npan : 256), block(kRpThreads);
   const bool q8 = a.C8 != nullptr;
+  if constexpr (!MX) {
+    if (a.h_blocked) {   // bf16 FFN down from gemm_xw's blocked hidden (no MXFP8 output in the bf16 mode)
+      if (q8) return hipErrorInvalidValue;
+      if (a.norm_w) hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, true, false, false, true>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, false, false, false, true>), grid, block, 0, st, a);
+      return hipGetLastError();
+    }
+  }
   if (a.norm_w) {
     if (q8) hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, true, true, MX>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((gemm_rp_kernel<WM, FM, true, false, MX>), grid, block, 0, st, a);
@@ -499,6 +511,7 @@ bool gemm_rp_accepts(const GemmArgs& a) {
     return false;
   if (a.rowscale || a.rpg || a.a_plane || a.c_plane || a.c2_plane || a.k_split || a.W3 || a.dw.w || a.att.probs)
     return false;
+  if (a.h_blocked && (a.lda % 32 || a.K > a.lda || a.C8)) return false;   // whole tiles; no MXFP8 output
   return !a.C8 || (a.C2 && a.C8s && a.ss8 && a.ldc == a.N);
 }
 
@@ -507,7 +520,7 @@ hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm) {
   RpArgs r{};
   r.A = a.A; r.lda = a.lda; r.W = a.W; r.bias = a.bias; r.R = a.R; r.ldr = a.ldr; r.C = a.C; r.ldc = a.ldc;
   r.C2 = a.C2; r.C8 = a.C8; r.C8s = a.C8s; r.ss8 = a.ss8; r.norm_w = a.norm_w; r.alpha = a.alpha;
-  r.M = a.M; r.K = a.K; r.dbg = a.dbg;
+  r.M = a.M; r.K = a.K; r.dbg = a.dbg; r.h_blocked = a.h_blocked;
   return launch_rp_bm<false>(r, bm, st);
 }
 

@@ -66,7 +66,9 @@ struct XwPos {
 // ping-pong schedule instead of the interleaved one (waves 0-3: half the K-steps, the whole VALU phase, the other
 // half; waves 4-7: VALU phase first), 128 (with 64) the waves 0-3 order for all waves.  Measured at M = 40960
 // (profiles/r04_xw_ablate.jsonl): the ping-pong is 7-8 % slower than the interleaved schedule.
-template <int EPI, bool RS, int DBG = 0>
+// HB: SWIGLU / GLU output in the blocked tile layout (common.h hblk_off): each 16-byte-per-lane store instruction
+// writes 1 KiB contiguous (lane l's chunk at 16 l of the tile half) instead of 32-byte segments of 32 rows
+template <int EPI, bool RS, int DBG = 0, bool HB = false>
 __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, int nc) {
   static_assert(EPI == EPI_SWIGLU || EPI == EPI_GLU || EPI == EPI_STORE, "SWIGLU / GLU / STORE");
   constexpr int kXwS = xw_stores<EPI>();
@@ -154,7 +156,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   // The accumulators start from bias x RMS (RS) or the bias, so acc x inv = A.W^T x inv + bias and the part reads
   // no LDS: a bias read here was the youngest LDS op at its use, i.e. an lgkmcnt(0) that also drained the W
   // fragment reads in flight
-  auto epi_part = [&](int b, int t, int64_t mrow, float inv, float cz, float inv2, int k) __attribute__((always_inline)) {
+  auto epi_part = [&](int b, int t, int64_t mrow, int blk, float inv, float cz, float inv2, int k) __attribute__((always_inline)) {
     if constexpr (EPI == EPI_STORE) {
       // output columns 64 t + u, + 1 (rows 0-31 of the tile) and 64 t + 32 + u, + 1 (rows 32-63)
       float y[2], z[2];
@@ -186,6 +188,8 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
       if ((k & 3) == 3) {   // registers 0-7 / 8-15 done: 8 consecutive hidden columns, one 16-byte store
         const xw_u32x4 w = {po[k - 3], po[k - 2], po[k - 1], po[k]};
         if constexpr ((DBG & 256) != 0) asm volatile("" ::"v"(w));   // no stores (timing only)
+        else if constexpr (HB)   // tile (blk, t) of the 32-row block / 32 hidden columns, half k >> 2, lane-contiguous
+          *reinterpret_cast<xw_u32x4*>(Cout + ((int64_t)blk * (p.ldc >> 5) + t) * 1024 + 512 * (k >> 2) + 8 * lane) = w;
         else *reinterpret_cast<xw_u32x4*>(Cout + mrow * p.ldc + 32 * t + 16 * (k >> 2) + 8 * lh) = w;
       }
     }
@@ -206,8 +210,10 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   int s = 0;
   float inv = 1.f, rms = 1.f;
   int64_t mrow = 0;
+  int mblk = 0;                                                   // the wave's 32-row block (HB tile row)
   int pt = 0;                                                     // previous step's W tile, row, row factor
   int64_t prow = 0;
+  int pblk = 0;
   float pinv = 1.f, pcz = -1.4426950408889634f, pinv2 = 1.f;   // previous step's row factor, inv * -log2 e, inv^2
 
   auto step = [&](auto Bc, auto Fc, auto Lc) __attribute__((always_inline)) {
@@ -232,6 +238,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
       rms = row_rms();
       inv = 1.0f / rms;
       mrow = min(cur.mt * kXwBM + wid * 32 + lr, p.M - 1);
+      mblk = cur.mt * (kXwBM / 32) + wid;
     }
     // every step DMAs a tile (the last two of the workgroup re-fetch their own into the free slot): a conditional DMA
     // or epilogue part is a branch around an LDS op, and at each such join the compiler's wait counter fell back to
@@ -281,7 +288,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
         }
         if constexpr ((DBG & 64) == 0) {   // interleaved schedule: DMA piece / epilogue part between the MFMAs
           if (dma_next && ks % 4 == 2) dma_piece(t2, sl2, ks / 4);
-          if (epi && ks % 3 == 1) epi_part(b ^ 1, pt, prow, pinv, pcz, pinv2, ks / 3);
+          if (epi && ks % 3 == 1) epi_part(b ^ 1, pt, prow, pblk, pinv, pcz, pinv2, ks / 3);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -290,7 +297,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
     auto valu_phase = [&]() __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        if (epi) epi_part(b ^ 1, pt, prow, pinv, pcz, pinv2, k);
+        if (epi) epi_part(b ^ 1, pt, prow, pblk, pinv, pcz, pinv2, k);
         if (k < kXwP && dma_next) dma_piece(t2, sl2, k);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -312,6 +319,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
     }
     pt = t;
     prow = mrow;
+    pblk = mblk;
     pinv = inv;
     pcz = inv * -1.4426950408889634f;
     pinv2 = inv * inv;
@@ -337,7 +345,7 @@ __global__ void __launch_bounds__(kXwWaves * 64, 1) gemm_xw_kernel(GemmArgs p, i
   }
   // the last step's epilogue (buffer 1: runs have even lengths)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) epi_part(1, pt, prow, pinv, pcz, pinv2, k);
+  for (int k = 0; k < 8; ++k) epi_part(1, pt, prow, pblk, pinv, pcz, pinv2, k);
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the re-fetch DMAs landed before the workgroup's LDS is released
 }
 
@@ -371,6 +379,13 @@ hipError_t launch_xw(const GemmArgs& a, int nc, hipStream_t st) {
     }
   }
 #endif
+  if constexpr (EPI == EPI_SWIGLU) {
+    if (a.h_blocked) {
+      if (a.rowscale) hipLaunchKernelGGL((gemm_xw_kernel<EPI, true, 0, true>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc);
+      else hipLaunchKernelGGL((gemm_xw_kernel<EPI, false, 0, true>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc);
+      return hipGetLastError();
+    }
+  }
   if (a.rowscale) hipLaunchKernelGGL((gemm_xw_kernel<EPI, true>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc);
   else hipLaunchKernelGGL((gemm_xw_kernel<EPI, false>), dim3(grid), dim3(kXwWaves * 64), 0, st, a, nc);
   return hipGetLastError();
@@ -383,6 +398,8 @@ hipError_t gemm_xw(const GemmArgs& a, int epi, int nc, hipStream_t st) {
   if (!a.a_bf16 || !a.c_bf16 || a.K != kXwK || a.N % kXwBN || a.N > kBiasMax || a.M <= 0 || a.rpg || a.lda % 8 ||
       a.ldc % 8 || a.k_split || a.C2)
     return hipErrorInvalidValue;
+  // the blocked hidden: SwiGLU only, whole 32-column tiles per row block (the caller pads the rows to 32)
+  if (a.h_blocked && (epi != EPI_SWIGLU || a.ldc % 32 || a.ldc < a.N / 2)) return hipErrorInvalidValue;
   const int nwt = a.N / kXwBN, ntm = (a.M + kXwBM - 1) / kXwBM;
   if (nc <= 0) nc = xw_run_length(ntm, nwt);
   if (nc < 2 || nc % 2 || nwt % nc) return hipErrorInvalidValue;   // runs of even length (see the kernel)

@@ -17,6 +17,7 @@ struct Knobs {
   int rp_norm;         // TONE_RP_NORM=0: norm_out as its own launch instead of inside FFN2 down (gemm_rp).  NOT
                        // bit-identical: the fused form adds the row's squares in another order and multiplies by one
                        // reciprocal per row instead of dividing each element (last-bit differences of the residual)
+  int h_blocked;       // TONE_H_BLOCKED=0: the bf16 FFN hidden row-major instead of in 32 x 32 tiles (bit-identical)
 };
 const Knobs& knobs();
 
@@ -83,6 +84,8 @@ struct GemmArgs {
   AttFuse att;        // EPI_RESID, K = 384 on gemm_sm only: A = ctx computed from P and V (A is not read)
   const float* norm_w; // EPI_RESID on the row-panel kernel only (gemm_rp): RMSNorm (gain norm_w) of each whole output
                        // row after the residual add; C and its shadows hold the normalized row
+  int h_blocked;       // bf16 FFN hidden h in 32 x 32 tiles (common.h hblk_off): the SWIGLU output C of gemm_xw, the
+                       // RESID input A of gemm_rp (the only two kernels that take it; gemm() routes it there or refuses)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);

@@ -33,6 +33,7 @@ const Knobs& knobs() {
     Knobs r;
     r.fp8_normq = env("TONE_FP8_NORMQ", 1) != 0;
     r.rp_norm = env("TONE_RP_NORM", 1) != 0;
+    r.h_blocked = env("TONE_H_BLOCKED", 1) != 0;
     return r;
   }();
   return k;
@@ -393,9 +394,10 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
               float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr,
               bool mx_out = false, const DwFuse* dw = nullptr, const AttFuse* att = nullptr,
-              const float* norm_w = nullptr) {
+              const float* norm_w = nullptr, bool h_blocked = false) {
   GemmArgs a{};   // value-initialised: every field not set below is zero
   a.norm_w = norm_w;
+  a.h_blocked = h_blocked;
   if (dw) a.dw = *dw;
   if (att) a.att = *att;
   a.A = A;
@@ -541,6 +543,9 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     // bf16 / fp8 modes: norm_out runs inside FFN2's down-projection when that launch is a row-panel one (whole rows);
     // in fp8 mode it then also emits the next layer's FFN1 operand
     const bool norm_fused = bf && knobs().rp_norm && gemm_rp_routed(M, kDff);
+    // bf16 mode, FFN up on gemm_xw and FFN down on gemm_rp (M >= 16384, 64+ blocks of 256 rows): the hidden h in 32 x 32
+    // tiles (common.h hblk_off), whole-KiB stores out of gemm_xw instead of 32-byte row segments
+    const bool h_blocked = bf && !f8 && knobs().h_blocked && gemm_rp_routed(M, kDff) && (M + 255) / 256 >= 40;
     const bool q8_after_norm = f8n && l != 6 && l < 14;
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
     // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
@@ -559,10 +564,10 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
                        0.5f, false, xs, nullptr, nullptr, fuse ? q8_after_norm : q8_fresh, fuse ? w.norm_out : nullptr);
       }
       CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[f], s->h, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
-                     1.0f, true, true));
+                     1.0f, true, true, nullptr, false, nullptr, nullptr, nullptr, h_blocked));
       // FFN2's down-projection on the row-panel kernel also applies the block-final RMSNorm (norm_out)
       return gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
-                       false, xs, false, nullptr, nullptr, f == 1 && norm_fused ? w.norm_out : nullptr);
+                       false, xs, false, nullptr, nullptr, f == 1 && norm_fused ? w.norm_out : nullptr, h_blocked);
     };
     CALL(ffn(0));
     // MHSA (conformer_blocks.py:816-825)
@@ -935,7 +940,9 @@ int finalize_weights(tone_session* s) {
   CALL(dalloc(s, reinterpret_cast<float**>(&s->flat), MB * kTMax * kSubOut));
   CALL(dalloc(s, &s->rA, MB * kTMax * D));
   CALL(dalloc(s, &s->rB, MB * kTrMax * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->h), MB * kTMax * kDff));
+  // h: rows padded to a multiple of 32 for the blocked layout (common.h hblk_off); bf16 in the bf16 mode, so this
+  // fp32-sized buffer holds it twice over
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->h), (MB * kTMax + 32) * kDff));
   CALL(dalloc(s, &s->qkv, MB * kTMax * 3 * D));
   CALL(dalloc(s, reinterpret_cast<float**>(&s->xn), MB * kTMax * D));
   CALL(dalloc(s, reinterpret_cast<float**>(&s->kv), MB * (30 + kTMax) * D));

@@ -161,6 +161,16 @@ __global__ void q8_cmp_kernel(const uint8_t* q, const uint8_t* s, const float* s
   atomicMax(reinterpret_cast<int*>(inv_err), __float_as_int(fabsf(a - b) / fabsf(b)));
 }
 
+// the blocked FFN hidden (common.h hblk_off; HBLK=1): row-major -> blocked and back, bf16 [rows][ld]
+__global__ void hblk_kernel(const uint16_t* src, uint16_t* dst, int64_t rows, int ld, int to_blocked) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * ld) return;
+  const int64_t r = i / ld;
+  const int c = (int)(i % ld);
+  if (to_blocked) dst[hblk_off(r, c, ld)] = src[i];
+  else dst[i] = src[hblk_off(r, c, ld)];
+}
+
 struct Q8Bufs {
   uint8_t *q = nullptr, *s = nullptr, *q2 = nullptr, *s2 = nullptr;
   float *ss = nullptr, *ss2 = nullptr, *inv_err = nullptr;
@@ -293,7 +303,7 @@ int main(int argc, char** argv) {
   void* C;
   CK(hipMalloc(&A, hA.size() * 2)); CK(hipMalloc(&W, hW.size() * 2));
   CK(hipMalloc(&bias, N * 4)); CK(hipMalloc(&R, hR.size() * 4));
-  CK(hipMalloc(&C, (size_t)M * nout * 4)); CK(hipMalloc(&C2, (size_t)M * nout * 2));
+  CK(hipMalloc(&C, ((size_t)M + 32) * nout * 4)); CK(hipMalloc(&C2, (size_t)M * nout * 2));
   CK(hipMalloc(&ref, (size_t)M * nout * 4)); CK(hipMalloc(&err, 4));
   const int64_t ws_cap = (int64_t)16 * M * N;
   CK(hipMalloc(&ws, ws_cap * 4));
@@ -373,6 +383,7 @@ int main(int argc, char** argv) {
   }
   float* refn = nullptr;
   if (normw) CK(hipMalloc(&refn, (size_t)M * nout * 4));
+  uint16_t *Ablk = nullptr, *Cun = nullptr;
   Q8Bufs q8b;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -404,6 +415,16 @@ int main(int argc, char** argv) {
     a.c_bf16 = f32 ? 0 : cbf;
     a.res16 = res16 && !f32;
     a.norm_w = (v >= 90 && v <= 98) ? normw : nullptr;
+    // HBLK=1: gemm_xw SWIGLU writes / gemm_rp reads the blocked hidden (checked through a row-major copy / built from one)
+    const bool hblk = getenv("HBLK") && atoi(getenv("HBLK")) && ((vv <= -300 && epi == 2) || (v >= 90 && v <= 98 && epi == 1));
+    a.h_blocked = hblk;
+    if (hblk && v >= 90) {
+      if (!Ablk) {
+        CK(hipMalloc(&Ablk, ((size_t)M + 32) * K * 2));
+        hipLaunchKernelGGL(hblk_kernel, dim3((unsigned)(((int64_t)M * K + 255) / 256)), dim3(256), 0, 0, A, Ablk, (int64_t)M, K, 1);
+      }
+      a.A = Ablk;
+    }
     const float* chk_ref = ref;
     if (a.norm_w && epi == 1) {   // the normalized reference (once per variant: cheap next to the fp32 reference)
       CK(hipMemcpy(refn, ref, (size_t)M * nout * 4, hipMemcpyDeviceToDevice));
@@ -435,7 +456,14 @@ int main(int argc, char** argv) {
     if (rc != hipSuccess) { printf("{\"variant\": %d, \"error\": \"%s\"}\n", v, hipGetErrorString(rc)); continue; }
     CK(hipDeviceSynchronize());
     CK(hipMemset(err, 0, 4));
-    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, C, a.res16 && epi <= 1 ? 2 : a.c_bf16, chk_ref, (int64_t)M * nout, err);
+    const void* Cchk = C;
+    if (hblk && vv <= -300) {   // the blocked output, back to row-major for the check
+      if (!Cun) CK(hipMalloc(&Cun, (size_t)M * nout * 2));
+      hipLaunchKernelGGL(hblk_kernel, dim3((unsigned)(((int64_t)M * nout + 255) / 256)), dim3(256), 0, 0,
+                         static_cast<const uint16_t*>(C), Cun, (int64_t)M, nout, 0);
+      Cchk = Cun;
+    }
+    hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, Cchk, a.res16 && epi <= 1 ? 2 : a.c_bf16, chk_ref, (int64_t)M * nout, err);
     float herr, herr2 = 0.f, q8_inv_err = 0.f;
     int q8_bad = -1;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
@@ -453,8 +481,9 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
-    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"shadow_err\": %.3g, \"norm\": %d, \"q8_bad\": %d, \"q8_inv_err\": %.3g}\n",
-           M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr, herr2, a.norm_w && epi == 1 ? 1 : 0, q8_bad, q8_inv_err);
+    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"shadow_err\": %.3g, \"norm\": %d, \"q8_bad\": %d, \"q8_inv_err\": %.3g, \"hblk\": %d}\n",
+           M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr, herr2, a.norm_w && epi == 1 ? 1 : 0, q8_bad, q8_inv_err,
+           (int)hblk);
     fflush(stdout);
   }
   return 0;

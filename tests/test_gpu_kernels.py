@@ -98,6 +98,24 @@ def test_xw_matches_reference(M, N, epi):
     assert r["max_rel_err"] < 1e-2, r
 
 
+@pytest.mark.parametrize("M", [40960, 20480, 16384])
+def test_xw_blocked_hidden_matches_reference(M):
+    """bf16 FFN up writing h in 32 x 32 tiles (common.h hblk_off, the session's layout from M = 16384): the output read
+    back through the inverse map equals the reference, i.e. every element lands where the consumer reads it."""
+    _gpu()
+    r = _run(M, 384, 3072, 2, -300, {"ROWSCALE": 1, "HBLK": 1})
+    assert r["hblk"] == 1 and r["max_rel_err"] < 1e-2, r
+
+
+@pytest.mark.parametrize("M", [40960, 20480, 16384])
+@pytest.mark.parametrize("norm", [0, 1])
+def test_rp_blocked_hidden_matches_reference(M, norm):
+    """bf16 FFN down (gemm_rp) reading h in 32 x 32 tiles, with and without the fused norm (FFN2 down)."""
+    _gpu()
+    r = _run(M, 1536, 384, 1, 90, {"RES16": 1, "HBLK": 1, "NORMW": norm})
+    assert r["hblk"] == 1 and r["max_rel_err"] < 3e-3 and r["shadow_err"] < 1.2e-2, r
+
+
 @pytest.mark.parametrize("M", [40960, 20480, 4096])
 def test_xs8_swiglu_matches_reference(M):
     """fp8 gemm_xs8 (FFN up SwiGLU with the MXFP8 quantization of h in its epilogue): the error is the MXFP8
