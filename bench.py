@@ -1,8 +1,10 @@
 """Throughput of the MI355X streaming acoustic path (BASELINE.json metric).
 
 A step = one streaming step (PCM chunk + carried state -> logprobs + next state) for every
-stream of the batch, inputs resident in HBM, states ping-ponged between two device slabs, the
-whole step replayed as one hipGraph.  With --gpus N (one process per GPU, torchrun) every rank
+stream of the batch, inputs resident in HBM, the state in the resident form a server keeps
+(conv caches in per-stream rings updated in place, the other sections ping-ponged between two
+slab rows; ``--state flat``: the boundary's (B, 219729) state ping-ponged between two buffers;
+bit-identical results), the whole step replayed as one hipGraph.  With --gpus N (one process per GPU, torchrun) every rank
 runs its own shard of streams (weak scaling, no data-path collective) and the per-step logprobs
 are all-gathered to every rank over RCCL (the host-decoding exchange).
 
@@ -218,7 +220,25 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
     fr = sess.frames
     rng = np.random.default_rng(1000 + rank)
     pcm = torch.from_numpy(synthetic_pcm(rng, B, args.chunks, chunk=chunk)).to(dev)   # (chunks, B, chunk)
-    slabs = [torch.zeros((B, C.STATE_SIZE), dtype=torch.float16, device=dev) for _ in range(2)]
+    ring = args.state == "ring"
+    if ring:
+        # the resident state a server keeps (include/tonehip.h tone_session_run_ring): the conv caches in per-stream rings
+        # updated in place, the other sections in two ping-pong rows per stream of one slab; imported from the zero state
+        slab = torch.zeros((2 * B, C.STATE_SIZE), dtype=torch.float16, device=dev)
+        rings = torch.zeros((B, sess.ring_elems), dtype=torch.float16, device=dev)
+        ids = torch.arange(B, dtype=torch.int32, device=dev)
+        rows = [ids, ids + B]
+        sess.ring_import(torch.zeros((B, C.STATE_SIZE), dtype=torch.float16, device=dev), slab, rows[0], rings, ids)
+        slabs = None
+    else:
+        slabs = [torch.zeros((B, C.STATE_SIZE), dtype=torch.float16, device=dev) for _ in range(2)]
+
+    def run_step(i: int, lp) -> None:
+        if ring:
+            sess.run_ring(signal, rows[i % 2], rows[(i + 1) % 2], slab, rings, ids, lp, stream=stream, check=False)
+        else:
+            sess.run(signal, slabs[i % 2], lp, slabs[(i + 1) % 2], stream=stream)
+
     signal = torch.empty((B, chunk), dtype=torch.int32, device=dev)   # audio lands here
     logp = [torch.zeros((cap, fr, C.VOCAB), dtype=torch.float32, device=dev) for _ in range(2)]
     gathered = [torch.empty((world * cap, fr, C.VOCAB), dtype=torch.float32, device=dev)
@@ -232,7 +252,7 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
         if freed[k] is not None:
             stream.wait_event(freed[k])
         signal.copy_(pcm[i % args.chunks], non_blocking=True)
-        sess.run(signal, slabs[k], logp[k][:B], slabs[1 - k], stream=stream)
+        run_step(i, logp[k][:B])
         if pg is not None:
             ready = stream.record_event()
             with torch.cuda.stream(comm):
@@ -282,7 +302,7 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
         with torch.cuda.stream(stream):
             for i in range(args.steps):
                 signal.copy_(pcm[i % args.chunks], non_blocking=True)
-                sess.run(signal, slabs[i % 2], logp[0][:B], slabs[(i + 1) % 2], stream=stream)
+                run_step(args.warmup + args.steps + i, logp[0][:B])
         torch.cuda.synchronize()
         per_stream = family_flops_per_stream(fr)
         fams = {}
@@ -354,6 +374,8 @@ def measure(args, B, precision, dev, local, world, rank, pg, with_roofline=True,
         res["roofline"] = roof
     sess.close()
     del slabs, pcm, logp, gathered
+    if ring:
+        del slab, rings
     torch.cuda.empty_cache()
     return res
 
@@ -526,6 +548,10 @@ def main() -> None:
                     help="headline leg's chunk: 2400 (300 ms, BASELINE) or 3200 (the 400 ms variant; A/B runs)")
     ap.add_argument("--cpu-baseline-s", type=float, default=8.0, help="CPU baseline budget per batch (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--state", choices=["ring", "flat"], default="ring",
+                    help="ring: the resident state form a server keeps (conv caches in per-stream rings updated in place, "
+                         "tone_session_run_ring); flat: the (B, 219729) boundary state ping-ponged between two buffers "
+                         "(tone_session_run).  Bit-identical results (tests/test_gpu_ring.py)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse N > 1 on one GPU (ranks share the card, collectives staged through host)")
     ap.add_argument("--alt", type=int, default=1, help="also measure BASELINE config 3 (bf16, B=2048) and the 400 ms "
@@ -640,6 +666,9 @@ def main() -> None:
             "config": {"workload": wl, "model": "T-one 71.7M (16-layer chunked Conformer, d384)",
                        "batch_per_gpu": cap, "global_batch": total, "chunk_ms": 300,
                        "parallelism": f"dp{world}", "graph": not args.no_graph,
+                       "state": ("resident: conv caches in per-stream rings updated in place, other sections in "
+                                 "ping-pong slab rows (run_ring)") if args.state == "ring"
+                       else "flat (B, 219729) fp16, ping-pong buffers (run)",
                        "collective": "RCCL all_gather_into_tensor of logprobs per step, overlapped" if pg is not None
                        else None},
             "chunks_per_s": round(chunks_s, 1),

@@ -29,6 +29,13 @@ SIGNATURES = {
     "tone_session_run": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int64, _c_void_p]),
     "tone_session_run_slots": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int64, _c_void_p, _c_int, _c_void_p]),
     "tone_session_run_rows": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int64, _c_void_p, _c_int, _c_void_p]),
+    "tone_session_run_ring": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int64, _c_void_p, _c_void_p,
+                                       _c_void_p, _c_int, _c_void_p]),
+    "tone_session_ring_import": (_c_int, [_c_void_p, _c_void_p, _c_int64, _c_void_p, _c_int64, _c_void_p, _c_void_p,
+                                          _c_void_p, _c_int, _c_void_p]),
+    "tone_session_ring_export": (_c_int, [_c_void_p, _c_void_p, _c_int64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                          _c_int64, _c_int, _c_void_p]),
+    "tone_session_ring_elems": (_c_int64, []),
     "tone_session_device_bytes": (_c_int64, [_c_void_p]),
     "tone_session_set_timing": (_c_int, [_c_void_p, _c_int]),
     "tone_session_kernel_us": (_c_double, [_c_void_p, _c_char_p, ctypes.POINTER(_c_int64)]),

@@ -87,15 +87,28 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // Where stream b's state rows live: row b of state_in / state_out, or rows slots[b] of device-resident
 // slabs; with slots_out, stream b reads row slots[b] and writes row slots_out[b] (ping-pong rows of one
 // slab, so streams that sit out a step keep their state without a copy).
+// Resident (ring) form, tone_session_run_ring: the conv-module caches of stream b live outside its row, in the ring
+// ring + ring_ids[b] * kRingElems, time-major [16 layers][30 frames][384 channels] fp16, updated in place: a step writes
+// only its T new frames, over the T oldest (the flat form rewrites all 30 shifted by T).  Cache frame i of layer l sits
+// at ring row (ph_l + i) mod 30, ph_l = (n T_l) mod 30, n = the stream's chunk counter mod 30, kept (as fp16) at the
+// first element of the row's then unused conv section; T_l = the layer's frames per step (T, or Tr in layers 7-14).
+constexpr int64_t kRingElems = (int64_t)16 * 30 * 384;   // 184320 = the flat conv section's size
+__host__ __device__ __forceinline__ int ring_phase(int n, int T) { return (n * T) % 30; }
+
 struct StateRef {
   const __half* in;
   __half* out;
   int64_t stride;          // elements between consecutive rows
   const int* slots;        // rows read (nullptr -> identity)
   const int* slots_out;    // rows written (nullptr -> the rows read)
+  __half* ring = nullptr;  // resident form: the conv rings (nullptr: flat form, caches in the rows)
+  const int* ring_ids = nullptr;   // ... and stream b's ring index
   __device__ __forceinline__ int64_t row_in(int b) const { return (int64_t)(slots ? slots[b] : b) * stride; }
   __device__ __forceinline__ int64_t row_out(int b) const {
     return slots_out ? (int64_t)slots_out[b] * stride : row_in(b);
+  }
+  __device__ __forceinline__ int chunk_counter(int b) const {   // resident form only
+    return (int)__half2float(in[row_in(b) + kOffConv]);
   }
 };
 

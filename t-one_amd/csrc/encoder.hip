@@ -460,9 +460,71 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g,
   }
 }
 
+// The same op on the resident form (common.h StateRef: the layer's 30 cached frames in the stream's ring, time-major
+// [30][384], frame i at ring row (ph + i) mod 30).  A thread takes a channel pair of one stream: every load and store is
+// a coalesced row segment (the flat form's [384][30] channel-major section needs the LDS staging above), and only the
+// T new frames are written back, over the T oldest (ring rows ph .. ph + T - 1), instead of the whole shifted window:
+// 30 + 3 T frames of HBM traffic per stream and layer instead of 60 + 2 T.  Arithmetic identical to dwconv_kernel
+// (same fma order, same SiLU forms): outputs and the exported state are bit-identical to the flat form's.
+template <int T, bool OBF>
+__global__ void __launch_bounds__(kD / 2) dwconv_ring_kernel(const void* __restrict__ g, StateRef s, int layer,
+                                                            const float* __restrict__ w, const float* __restrict__ bias,
+                                                            void* __restrict__ out) {
+  const int b = blockIdx.x, c = 2 * threadIdx.x;
+  const int ph = ring_phase(s.chunk_counter(b), T);
+  __half* rg = s.ring + (int64_t)s.ring_ids[b] * kRingElems + (int64_t)layer * kConvS * kD + c;
+  float x[kConvS + T][2];
+#pragma unroll
+  for (int i = 0; i < kConvS; ++i) {
+    const int r = ph + i < kConvS ? ph + i : ph + i - kConvS;
+    const __half2 h = *reinterpret_cast<const __half2*>(rg + (int64_t)r * kD);
+    x[i][0] = __low2float(h);
+    x[i][1] = __high2float(h);
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int64_t gi = ((int64_t)b * T + t) * kD + c;
+    x[kConvS + t][0] = load_act<OBF>(g, gi);
+    x[kConvS + t][1] = load_act<OBF>(g, gi + 1);
+  }
+  float wr[kConvK][2];
+#pragma unroll
+  for (int k = 0; k < kConvK; ++k) {
+    const float2 wv = *reinterpret_cast<const float2*>(w + k * kD + c);
+    wr[k][0] = wv.x;
+    wr[k][1] = wv.y;
+  }
+  const float2 bb = *reinterpret_cast<const float2*>(bias + c);
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    float y[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float acc = e ? bb.y : bb.x;
+#pragma unroll
+      for (int k = 0; k < kConvK; ++k) acc = fmaf(wr[k][e], x[t + k][e], acc);
+      if constexpr (OBF) y[e] = acc * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc * -1.4426950408889634f));
+      else y[e] = silu_f(acc);
+    }
+    const int64_t oi = ((int64_t)b * T + t) * kD + c;
+    store_act<OBF>(out, oi, y[0]);
+    store_act<OBF>(out, oi + 1, y[1]);
+  }
+  // the T new frames over the T oldest: ring rows ph .. ph + T - 1 (mod 30)
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const int r = ph + j < kConvS ? ph + j : ph + j - kConvS;
+    *reinterpret_cast<__half2*>(rg + (int64_t)r * kD) = __floats2half2_rn(x[kConvS + j][0], x[kConvS + j][1]);
+  }
+}
+
 template <int T, bool OBF>
 static hipError_t launch_dwconv_t(const void* g, StateRef s, int layer, const float* w, const float* b, void* out,
                                   int B, hipStream_t st) {
+  if (s.ring) {
+    hipLaunchKernelGGL((dwconv_ring_kernel<T, OBF>), dim3(B), dim3(kD / 2), 0, st, g, s, layer, w, b, out);
+    return hipGetLastError();
+  }
   // block shape by batch: 192 channels x 1 stream from B = 1024, else 128 x 1 (profiles/r01_dwconv_sweep.txt,
   // r03_dwconv_sweep.txt)
   if (B >= 1024)
@@ -679,6 +741,63 @@ __global__ void __launch_bounds__(256) head_rows_kernel(const void* __restrict__
     const float sil = expf(acc[kVocab - 2] - m - lse) + expf(acc[kVocab - 1] - m - lse);
     frame_info[row] = tok | ((sil <= kSilenceThreshold) ? 256 : 0);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Flat state <-> resident form (common.h StateRef).  Import: flat row i -> slab row rows[i] (every section but conv, whose
+// first element becomes the chunk counter 0) and ring ring_ids[i] (phase 0: ring row i of layer l = cache frame i).
+// Export: the inverse, with each layer's phase from the counter and the layer's frames per step (T, or Tr in 7-14).
+// One workgroup per stream; plain copies (bit-exact).
+__global__ void __launch_bounds__(256) ring_import_kernel(const __half* __restrict__ flat, int64_t fstride,
+                                                          __half* __restrict__ slab, int64_t sstride,
+                                                          const int* __restrict__ rows, __half* __restrict__ ring,
+                                                          const int* __restrict__ ring_ids) {
+  const int i = blockIdx.x;
+  const __half* f = flat + (int64_t)i * fstride;
+  __half* r = slab + (int64_t)rows[i] * sstride;
+  __half* rg = ring + (int64_t)ring_ids[i] * kRingElems;
+  for (int64_t e = threadIdx.x; e < kStateSize; e += 256) {
+    if (e < kOffConv || e >= kOffConv + kRingElems) r[e] = f[e];
+    else if (e == kOffConv) r[e] = __float2half_rn(0.f);
+  }
+  // ring[l][t][c] = flat conv[l][c][t]
+  for (int64_t e = threadIdx.x; e < kRingElems; e += 256) {
+    const int c = (int)(e % kD), t = (int)((e / kD) % kConvS), l = (int)(e / (kD * kConvS));
+    rg[e] = f[kOffConv + ((int64_t)l * kD + c) * kConvS + t];
+  }
+}
+
+__global__ void __launch_bounds__(256) ring_export_kernel(const __half* __restrict__ slab, int64_t sstride,
+                                                          const int* __restrict__ rows, const __half* __restrict__ ring,
+                                                          const int* __restrict__ ring_ids, __half* __restrict__ flat,
+                                                          int64_t fstride, int T, int Tr) {
+  const int i = blockIdx.x;
+  const __half* r = slab + (int64_t)rows[i] * sstride;
+  __half* f = flat + (int64_t)i * fstride;
+  const __half* rg = ring + (int64_t)ring_ids[i] * kRingElems;
+  const int n = (int)__half2float(r[kOffConv]);
+  for (int64_t e = threadIdx.x; e < kStateSize; e += 256)
+    if (e < kOffConv || e >= kOffConv + kRingElems) f[e] = r[e];
+  // flat conv[l][c][t] = ring[l][(ph_l + t) mod 30][c]
+  for (int64_t e = threadIdx.x; e < kRingElems; e += 256) {
+    const int t = (int)(e % kConvS), c = (int)((e / kConvS) % kD), l = (int)(e / (kD * kConvS));
+    const int ph = ring_phase(n, (l > 6 && l <= 14) ? Tr : T);
+    f[kOffConv + e] = rg[((int64_t)l * kConvS + (ph + t) % kConvS) * kD + c];
+  }
+}
+
+hipError_t launch_ring_import(const __half* flat, int64_t fstride, __half* slab, int64_t sstride, const int* rows, __half* ring,
+                              const int* ring_ids, int n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ring_import_kernel, dim3(n), dim3(256), 0, st, flat, fstride, slab, sstride, rows, ring, ring_ids);
+  return hipGetLastError();
+}
+
+hipError_t launch_ring_export(const __half* slab, int64_t sstride, const int* rows, const __half* ring, const int* ring_ids,
+                              __half* flat, int64_t fstride, int T, int Tr, int n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ring_export_kernel, dim3(n), dim3(256), 0, st, slab, sstride, rows, ring, ring_ids, flat, fstride, T, Tr);
+  return hipGetLastError();
 }
 
 hipError_t launch_head(const void* x, const float* w, const float* b, float* logp, int32_t* frame_info, int rows, bool r16,

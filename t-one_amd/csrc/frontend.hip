@@ -33,6 +33,8 @@ __global__ void __launch_bounds__(256) mel_prep_kernel(const int32_t* __restrict
   if (i == 0) {   // mhsa_len + T: EncoderState.state_keep_size = the chunk's frame count (conformer_blocks.py:206)
     const float ml = __half2float(s.in[srow + kOffMhsaLen]);
     s.out[orow + kOffMhsaLen] = __float2half_rn(fminf(ml + (float)T, (float)kMhsaS));
+    // resident form: the chunk counter (mod 30) that sets the conv rings' phases (common.h StateRef)
+    if (s.ring) s.out[orow + kOffConv] = __float2half_rn((float)((s.chunk_counter(b) + 1) % kConvS));
   }
 }
 

@@ -241,8 +241,16 @@ struct AttnArgs {
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 
 // a9: depthwise causal conv k31 with carried state + folded BatchNorm + SiLU; g and out bf16 when obf, else fp32.
+// With s.ring (the resident form) the caches are read from / the new frames written to the stream's ring.
 hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
                          int T, int B, hipStream_t st);
+
+// flat state <-> resident form (common.h StateRef, tone_session_ring_import / _export): stream i's flat row i <-> slab
+// row rows[i] + ring ring_ids[i]; T / Tr = frames per step outside / inside the reduced block (the layers' phases)
+hipError_t launch_ring_import(const __half* flat, int64_t fstride, __half* slab, int64_t sstride, const int* rows, __half* ring,
+                              const int* ring_ids, int n, hipStream_t st);
+hipError_t launch_ring_export(const __half* slab, int64_t sstride, const int* rows, const __half* ring, const int* ring_ids,
+                              __half* flat, int64_t fstride, int T, int Tr, int n, hipStream_t st);
 
 // a11: reduction state + grouped conv (384->1536, k3, s2) -> y [B*5][1536]; x fp16 (residual stream) when obf
 hipError_t launch_reduce_conv(const void* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,

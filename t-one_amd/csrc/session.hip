@@ -133,7 +133,7 @@ struct tone_session {
   // graphs
   struct GraphKey {
     int batch;
-    const void *a, *b, *c, *d, *e, *f, *g;
+    const void *a, *b, *c, *d, *e, *f, *g, *h, *i;
     int64_t stride;
     bool operator<(const GraphKey& o) const {
       return std::memcmp(this, &o, sizeof(GraphKey)) < 0;
@@ -644,7 +644,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     q8_fresh = false;
     // Convolution module (conformer_blocks.py:827-830)
     // fp32 mode at M <= 64 (the drop-in's per-call batch): the depthwise conv runs in pw1's epilogue (gemm_sm.hip)
-    if (s->precision == TONE_PRECISION_FP32 && M <= 64 && s->w3.count(w.wpw1)) {
+    // (not with the resident state: the fused form reads the flat conv section)
+    if (s->precision == TONE_PRECISION_FP32 && M <= 64 && s->w3.count(w.wpw1) && !sr.ring) {
       const DwFuse dw{w.wdw, w.bdw, sr, l, T, static_cast<float*>(s->d)};
       CALL(gemm_call(s, st, "gemm_pw1_dwconv", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f,
                      false, false, nullptr, false, &dw));
@@ -978,6 +979,7 @@ int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp,
   if (!signal || !sr.in || !sr.out || !logp) return fail(TONE_E_INVALID, "null I/O pointer");
   if (sr.stride < kStateSize) return fail(TONE_E_INVALID, "state stride < 219729");
   if (sr.in == sr.out && !sr.slots_out) return fail(TONE_E_INVALID, "state_out must not alias state_in");
+  if (sr.ring && !sr.ring_ids) return fail(TONE_E_INVALID, "null ring ids");
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
   // graphs replay a captured step keyed by (batch, I/O pointers); debug stops and timing run eagerly
@@ -992,6 +994,8 @@ int run_common(tone_session* s, const int32_t* signal, StateRef sr, float* logp,
     k.e = sr.slots;
     k.f = s->frame_info;
     k.g = sr.slots_out;
+    k.h = sr.ring;
+    k.i = sr.ring_ids;
     k.stride = sr.stride;
     (void)key_a;
     (void)key_b;
@@ -1136,6 +1140,42 @@ int tone_session_run_rows(tone_session* s, const int32_t* signal, const int32_t*
   StateRef sr{reinterpret_cast<const __half*>(slab), reinterpret_cast<__half*>(slab), slab_stride, rows_in, rows_out};
   return run_common(s, signal, sr, logprobs, batch, stream, nullptr, nullptr);
 }
+
+int tone_session_run_ring(tone_session* s, const int32_t* signal, const int32_t* rows_in, const int32_t* rows_out,
+                          uint16_t* slab, int64_t slab_stride, uint16_t* rings, const int32_t* ring_ids, float* logprobs,
+                          int batch, void* stream) {
+  if (!rows_in || !rows_out || !rings || !ring_ids) return fail(TONE_E_INVALID, "null rows / rings / ring ids");
+  if (rows_in == rows_out) return fail(TONE_E_INVALID, "rows_out must differ from rows_in");
+  StateRef sr{reinterpret_cast<const __half*>(slab), reinterpret_cast<__half*>(slab), slab_stride, rows_in, rows_out,
+              reinterpret_cast<__half*>(rings), ring_ids};
+  return run_common(s, signal, sr, logprobs, batch, stream, nullptr, nullptr);
+}
+
+int tone_session_ring_import(tone_session* s, const uint16_t* flat, int64_t flat_stride, uint16_t* slab, int64_t slab_stride,
+                             const int32_t* rows, uint16_t* rings, const int32_t* ring_ids, int n, void* stream) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  if (!flat || !slab || !rows || !rings || !ring_ids || n < 0) return fail(TONE_E_INVALID, "bad ring_import arguments");
+  if (flat_stride < kStateSize || slab_stride < kStateSize) return fail(TONE_E_INVALID, "state stride < 219729");
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(launch_ring_import(reinterpret_cast<const __half*>(flat), flat_stride, reinterpret_cast<__half*>(slab), slab_stride,
+                             rows, reinterpret_cast<__half*>(rings), ring_ids, n, static_cast<hipStream_t>(stream)));
+  return TONE_OK;
+}
+
+int tone_session_ring_export(tone_session* s, const uint16_t* slab, int64_t slab_stride, const int32_t* rows,
+                             const uint16_t* rings, const int32_t* ring_ids, uint16_t* flat, int64_t flat_stride, int n,
+                             void* stream) {
+  if (!s) return fail(TONE_E_INVALID, "null session");
+  if (!flat || !slab || !rows || !rings || !ring_ids || n < 0) return fail(TONE_E_INVALID, "bad ring_export arguments");
+  if (flat_stride < kStateSize || slab_stride < kStateSize) return fail(TONE_E_INVALID, "state stride < 219729");
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(launch_ring_export(reinterpret_cast<const __half*>(slab), slab_stride, rows, reinterpret_cast<const __half*>(rings),
+                             ring_ids, reinterpret_cast<__half*>(flat), flat_stride, s->geo.T, s->geo.Tr, n,
+                             static_cast<hipStream_t>(stream)));
+  return TONE_OK;
+}
+
+int64_t tone_session_ring_elems(void) { return kRingElems; }
 
 int64_t tone_session_device_bytes(const tone_session* s) { return s ? s->dev_bytes : 0; }
 

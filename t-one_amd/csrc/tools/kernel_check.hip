@@ -16,13 +16,15 @@
 // the measure for recomputed values, whose ulp distance near zero says nothing).
 //
 // Prints one JSON line: {"check", "B", "T", outputs: {name: max |out - ref| / (1 + |ref|)}, "nan", "state_ulp",
-// "state_sentinel_bad", "state_in_changed", "us"}.
+// "state_err", "state_sentinel_bad", "state_in_changed", "us" (the launch's mean time over 20 warm repeats, measured
+// after the checks)}.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <functional>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -271,19 +273,29 @@ struct Report {
   }
 };
 
+// the launch under test: run once here (the checks compare its outputs); Report::print times it afterwards (3 warm-up
+// launches, then the mean of 20), when the results have been read -- later launches may change the state they read
+static std::function<hipError_t()> g_launch;
 template <typename F>
-static double time_once(F&& f) {   // launch + sync, wall time of the launch (the check runs it once)
+static double time_once(F&& f) {
+  g_launch = f;
+  CK(f());
+  CK(hipDeviceSynchronize());
+  return 0.0;
+}
+static double time_warm() {
+  if (!g_launch) return 0.0;
+  for (int i = 0; i < 3; ++i) CK(g_launch());
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   CK(hipEventRecord(a, 0));
-  CK(f());
+  for (int i = 0; i < 20; ++i) CK(g_launch());
   CK(hipEventRecord(b, 0));
   CK(hipEventSynchronize(b));
   float ms = 0.f;
   CK(hipEventElapsedTime(&ms, a, b));
-  CK(hipDeviceSynchronize());
-  return ms * 1e3;
+  return ms * 1e3 / 20;
 }
 
 static dim3 grid1(int64_t n, int bs = 256) { return dim3((unsigned)((n + bs - 1) / bs)); }
@@ -447,7 +459,7 @@ static void check_pre(const std::string& which, int B, int chunk, bool bf, Repor
 
   if (which == "sub_conv") {   // bf16, 300 ms: the flat conv2 output
     uint16_t* flat = pool.get<uint16_t>((int64_t)B * T * kSubOut);
-    rep.us = time_once([&] {
+    rep.us = time_once([=] {
       return launch_sub_conv_bf16(feats, sl.ref(), pw, w1td, sc1, sh1, w2cd, sc2, sh2, flat, B, 0);
     });
     float* fr = pool.get<float>((int64_t)B * T * kSubOut);
@@ -456,7 +468,7 @@ static void check_pre(const std::string& which, int B, int chunk, bool bf, Repor
     rep.out("flat", flat, 1, kSubOut, fr, (int64_t)B * T, kSubOut);
   } else {                     // sub1: x2 (the conv2 input) in HBM
     void* x2 = bf ? (void*)pool.get<uint16_t>((int64_t)B * IN * kSub1F * kSub1C) : (void*)pool.get<float>((int64_t)B * IN * kSub1F * kSub1C);
-    rep.us = time_once([&] { return launch_sub1(feats, sl.ref(), pw, w1, w1td, sc1, sh1, x2, bf, B, chunk, 0); });
+    rep.us = time_once([=] { return launch_sub1(feats, sl.ref(), pw, w1, w1td, sc1, sh1, x2, bf, B, chunk, 0); });
     rep.out("x2", x2, bf ? 1 : 0, (int64_t)kSub1F * kSub1C, x2r, (int64_t)B * IN, kSub1F * kSub1C);
   }
   rep.state(sl, secs, exps);
@@ -488,7 +500,7 @@ static void check_conv2(int B, int chunk, bool bf, Report& rep) {
     CK(hipMemcpy(w2cd, w2c.data(), w2c.size() * 2, hipMemcpyHostToDevice));
     uint16_t* x2 = to_bf16(x2f, nx);
     uint16_t* flat = pool.get<uint16_t>((int64_t)B * T * kSubOut);
-    rep.us = time_once([&] { return conv2_gemm(x2, w2cd, sc, sh, flat, B, true, 0, chunk, nullptr); });
+    rep.us = time_once([=] { return conv2_gemm(x2, w2cd, sc, sh, flat, B, true, 0, chunk, nullptr); });
     rep.out("flat", flat, 1, kSubOut, fr, (int64_t)B * T, kSubOut);
     return;
   }
@@ -507,7 +519,7 @@ static void check_conv2(int B, int chunk, bool bf, Report& rep) {
   uint16_t* w2p = pool.get<uint16_t>(px.size());
   CK(hipMemcpy(w2p, px.data(), px.size() * 2, hipMemcpyHostToDevice));
   float* flat = pool.get<float>((int64_t)B * T * kSubOut);
-  rep.us = time_once([&] { return conv2_gemm(x2f, w2, sc, sh, flat, B, false, 0, chunk, w2p); });
+  rep.us = time_once([=] { return conv2_gemm(x2f, w2, sc, sh, flat, B, false, 0, chunk, w2p); });
   rep.out("flat", flat, 0, kSubOut, fr, (int64_t)B * T, kSubOut);
 }
 
@@ -550,9 +562,74 @@ static void check_dwconv(int B, int T, bool bf, Report& rep) {
   hipLaunchKernelGGL(ref_dwconv_kernel, grid1((int64_t)B * kD), dim3(256), 0, 0, g, bf ? 1 : 0, sl.ref(), layer, w, bias, T,
                      ref, exps, B);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([&] { return launch_dwconv(g, sl.ref(), layer, w, bias, out, bf, T, B, 0); });
+  rep.us = time_once([=] { return launch_dwconv(g, sl.ref(), layer, w, bias, out, bf, T, B, 0); });
   rep.out("out", out, bf ? 1 : 0, kD, ref, M, kD);
   rep.state(sl, secs, exps);
+}
+
+__global__ void cmp_bytes_kernel(const uint8_t* a, const uint8_t* b, int64_t n, int* bad);
+
+// the resident form (common.h StateRef ring): stream b's counter n_b = (7 b + 3) mod 30 in its read row, its ring
+// ring_ids[b] = a shuffle of B + 1 rings; the reference reads cache frame i at ring row (n_b T + i) mod 30 and writes the
+// expected ring (the T new frames over rows (n_b T + j) mod 30, j < T) into a copy of the rings
+__global__ void set_counter_kernel(StateRef s, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) const_cast<__half*>(s.in)[s.row_in(b) + kOffConv] = __float2half_rn((float)((7 * b + 3) % kConvS));
+}
+__global__ void ref_dwconv_ring_kernel(const void* g, int gty, StateRef s, const __half* ring0, int layer, const float* w,
+                                       const float* bias, int T, float* out, __half* ring_exp, int B) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * kD) return;
+  const int b = (int)(i / kD), c = (int)(i % kD);
+  const int n = (7 * b + 3) % kConvS, ph = (n * T) % kConvS;
+  const int64_t base = (int64_t)s.ring_ids[b] * kRingElems + (int64_t)layer * kConvS * kD + c;
+  float x[kConvS + kTMax];
+  for (int k = 0; k < kConvS; ++k) x[k] = h2f(ring0[base + (int64_t)((ph + k) % kConvS) * kD]);
+  for (int t = 0; t < T; ++t) x[kConvS + t] = load_typed(g, gty, ((int64_t)b * T + t) * kD + c);
+  for (int t = 0; t < T; ++t) {
+    double acc = bias[c];
+    for (int k = 0; k < kConvK; ++k) acc += (double)w[k * kD + c] * x[t + k];
+    out[((int64_t)b * T + t) * kD + c] = (float)(acc / (1.0 + exp(-acc)));
+  }
+  for (int j = 0; j < T; ++j) ring_exp[base + (int64_t)((ph + j) % kConvS) * kD] = __float2half_rn(x[kConvS + j]);
+}
+
+static void check_dwconv_ring(int B, int T, bool bf, Report& rep) {
+  Slab sl;
+  sl.make(B);
+  const int layer = 9, nr = B + 1;
+  std::vector<int> ids(B);
+  for (int b = 0; b < B; ++b) ids[b] = (int)(((int64_t)5 * b + 1) % nr);   // 5 coprime with B + 1 for the tested B
+  int* dids = pool.get<int>(B);
+  CK(hipMemcpy(dids, ids.data(), B * 4, hipMemcpyHostToDevice));
+  StateRef sr = sl.ref();
+  sr.ring = to_f16(rand_f32((int64_t)nr * kRingElems, 34, 1.f), (int64_t)nr * kRingElems);
+  sr.ring_ids = dids;
+  hipLaunchKernelGGL(set_counter_kernel, grid1(B), dim3(256), 0, 0, sr, B);
+  __half* ring0 = pool.get<__half>((int64_t)nr * kRingElems);
+  __half* ring_exp = pool.get<__half>((int64_t)nr * kRingElems);
+  CK(hipMemcpy(ring0, sr.ring, (size_t)nr * kRingElems * 2, hipMemcpyDeviceToDevice));
+  CK(hipMemcpy(ring_exp, sr.ring, (size_t)nr * kRingElems * 2, hipMemcpyDeviceToDevice));
+  const int64_t M = (int64_t)B * T;
+  float* gf = rand_f32(M * kD, 31, 1.5f, 0.f, bf);
+  const void* g = bf ? (const void*)to_bf16(gf, M * kD) : (const void*)gf;
+  const float* w = rand_f32(kConvK * kD, 32, 0.2f);
+  const float* bias = rand_f32(kD, 33, 0.2f);
+  void* out = bf ? (void*)pool.get<uint16_t>(M * kD) : (void*)pool.get<float>(M * kD);
+  float* ref = pool.get<float>(M * kD);
+  hipLaunchKernelGGL(ref_dwconv_ring_kernel, grid1((int64_t)B * kD), dim3(256), 0, 0, g, bf ? 1 : 0, sr, ring0, layer, w, bias,
+                     T, ref, ring_exp, B);
+  CK(hipDeviceSynchronize());
+  rep.us = time_once([=] { return launch_dwconv(g, sr, layer, w, bias, out, bf, T, B, 0); });
+  rep.out("out", out, bf ? 1 : 0, kD, ref, M, kD);
+  // every ring element (all layers, the unused ring too) against the expected rings: bytes
+  int* bad = pool.get<int>(1);
+  CK(hipMemset(bad, 0, 4));
+  hipLaunchKernelGGL(cmp_bytes_kernel, dim3(2048), dim3(256), 0, 0, reinterpret_cast<const uint8_t*>(sr.ring),
+                     reinterpret_cast<const uint8_t*>(ring_exp), (int64_t)nr * kRingElems * 2, bad);
+  int hb = 0;
+  CK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
+  rep.outs.emplace_back("ring_bad_bytes", Res{(float)hb, 0, 0, 0, 0, 0});
 }
 
 // =====================================================================================================================
@@ -704,7 +781,7 @@ static void check_attention(int B, int T, int S, bool recompute, bool bf, Report
   hipLaunchKernelGGL(ref_attention_kernel, grid1((int64_t)B * kHeads * T, 64), dim3(64), 0, 0, ar, ty, ref,
                      recompute && a.probs ? probs_ref : nullptr);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([&] { return launch_attention(a, 0); });
+  rep.us = time_once([=] { return launch_attention(a, 0); });
   rep.out("ctx", ctx, ty, kD, ref, (int64_t)B * T, kD);
   if (recompute && a.probs) rep.out("probs", a.probs, 0, TK, probs_ref, (int64_t)B * kHeads * T, TK);
   // the attention kernels read the state (mhsa_len) and write none of it
@@ -766,7 +843,7 @@ static void check_kv(int B, int T, int S, bool bf, Report& rep) {
   hipLaunchKernelGGL(ref_kv_kernel, grid1((int64_t)B * kD), dim3(256), 0, 0, r, bf ? 2 : 0, nw, sl.ref(), slot, T, S, xr, kr,
                      exps, B);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([&] { return launch_kv_assemble(r, nw, sl.ref(), slot, T, S, xn, kv, bf, B, 0); });
+  rep.us = time_once([=] { return launch_kv_assemble(r, nw, sl.ref(), slot, T, S, xn, kv, bf, B, 0); });
   rep.out("xn", xn, bf ? 1 : 0, kD, xr, M, kD);
   rep.out("kv", kv, bf ? 1 : 0, kD, kr, (int64_t)B * TK, kD);
   rep.state(sl, secs, exps);
@@ -811,7 +888,7 @@ static void check_reduce(int B, int T, bool bf, Report& rep) {
   hipLaunchKernelGGL(ref_reduce_kernel, grid1((int64_t)B * 4 * kD), dim3(256), 0, 0, x, bf ? 2 : 0, sl.ref(), w, bias, T, yr,
                      exps, B);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([&] { return launch_reduce_conv(x, sl.ref(), w, bias, y, bf, B, T, 0); });
+  rep.us = time_once([=] { return launch_reduce_conv(x, sl.ref(), w, bias, y, bf, B, T, 0); });
   rep.out("y", y, bf ? 1 : 0, 4 * kD, yr, (int64_t)B * TR, 4 * kD);
   rep.state(sl, secs, exps);
 }
@@ -846,7 +923,7 @@ static void check_upsample(int B, int T, bool r16, Report& rep) {
   const void* x5 = r16 ? (const void*)to_f16(c, n5) : (const void*)c;
   uint16_t* shadow = pool.get<uint16_t>(n10);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([&] { return launch_upsample_add(x10, x5, B, T, shadow, 0, r16, 0); });
+  rep.us = time_once([=] { return launch_upsample_add(x10, x5, B, T, shadow, 0, r16, 0); });
   rep.out("x", x10, r16 ? 2 : 0, kD, ref, (int64_t)B * T, kD);
   rep.out("shadow", shadow, 1, kD, ref, (int64_t)B * T, kD);
 }
@@ -904,7 +981,7 @@ static void check_head(int rows, bool r16, Report& rep) {
   int32_t* ok = pool.get<int32_t>(rows);
   hipLaunchKernelGGL(ref_head_kernel, grid1(rows), dim3(256), 0, 0, x, r16 ? 2 : 0, w, b, lr, fr, ok, rows);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([&] { return launch_head(x, w, b, lp, fi, rows, r16, 0); });
+  rep.us = time_once([=] { return launch_head(x, w, b, lp, fi, rows, r16, 0); });
   rep.out("logprobs", lp, 0, kVocab, lr, rows, kVocab);
   int* bad = pool.get<int>(1);
   CK(hipMemset(bad, 0, 4));
@@ -954,7 +1031,7 @@ static void check_rmsnorm(int rows, bool r16, bool q8, Report& rep) {
     ss = pool.get<float>((int64_t)rows * kSsSlots);
   }
   CK(hipDeviceSynchronize());
-  rep.us = time_once([&] { return launch_rmsnorm(x, w, rows, shadow, 0, r16, 0, q, s, ss); });
+  rep.us = time_once([=] { return launch_rmsnorm(x, w, rows, shadow, 0, r16, 0, q, s, ss); });
   rep.out("x", x, r16 ? 2 : 0, kD, ref, rows, kD);
   rep.out("shadow", shadow, 1, kD, ref, rows, kD);
   if (q8) {
@@ -1006,6 +1083,7 @@ int main(int argc, char** argv) {
   else if (ck == "conv2_f32") check_conv2(B, 2400, false, rep);
   else if (ck == "conv2_f32_400") check_conv2(B, 3200, false, rep);
   else if (ck == "conv2_bf16_400") check_conv2(B, 3200, true, rep);
+  else if (ck.rfind("dwconv_ring", 0) == 0) check_dwconv_ring(B, T, bf, rep);
   else if (ck.rfind("dwconv", 0) == 0) check_dwconv(B, T, bf, rep);
   else if (ck.rfind("attn_rec", 0) == 0) check_attention(B, T, S, true, bf, rep);
   else if (ck.rfind("attn_shared", 0) == 0) check_attention(B, T, 0, false, bf, rep);
@@ -1019,6 +1097,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   if (ck == "sub_conv" || ck.rfind("sub1", 0) == 0 || ck.rfind("conv2", 0) == 0) rep.T = ck.find("400") != std::string::npos ? 13 : kT;
+  rep.us = time_warm();
   rep.print();
   return 0;
 }

@@ -169,6 +169,82 @@ class ToneSession:
                                                    slab.data_ptr(), slab.stride(0), logprobs.data_ptr(), b, st),
                    "tone_session_run_rows")
 
+    # --- resident state: conv caches in per-stream rings (include/tonehip.h tone_session_run_ring) ----------------
+    @property
+    def ring_elems(self) -> int:
+        """fp16 elements of one stream's conv ring (16 x 30 x 384)."""
+        return int(self._lib.tone_session_ring_elems())
+
+    def _check_ring_args(self, b, slab, rings, ids, *row_lists):
+        torch = _torch()
+        for t, dt in ((slab, torch.float16), (rings, torch.float16), (ids, torch.int32)) + tuple((r, torch.int32) for r in row_lists):
+            if t.dtype != dt or t.device != self.dev:
+                raise ValueError(f"expected {dt} tensor on {self.dev}, got {t.dtype} on {t.device}")
+        for r in (ids,) + row_lists:
+            if tuple(r.shape) != (b,) or not r.is_contiguous():
+                raise ValueError(f"rows / ring ids must be contiguous (B,) = ({b},) int32 tensors, got {tuple(r.shape)}")
+        if slab.dim() != 2 or slab.stride(1) != 1 or slab.stride(0) < C.STATE_SIZE or slab.shape[1] < C.STATE_SIZE:
+            raise ValueError("slab must be (n_rows, >= 219729) fp16 with unit column stride")
+        if rings.dim() != 2 or rings.shape[1] != self.ring_elems or not rings.is_contiguous():
+            raise ValueError(f"rings must be a contiguous (n_rings, {self.ring_elems}) fp16 tensor")
+
+    def run_ring(self, signal, rows_in, rows_out, slab, rings, ring_ids, logprobs, stream=None, check: bool = True) -> None:
+        """Step on the resident state: the non-conv sections ping-pong between rows rows_in[i] / rows_out[i] of
+        ``slab`` (as run_rows), stream i's conv caches live in ring ring_ids[i] of ``rings`` (n_rings, ring_elems)
+        and are updated in place.  Convert with ring_import / ring_export.  With ``check`` the ids are range- and
+        distinctness-checked (one device sync)."""
+        torch = _torch()
+        b = int(signal.shape[0])
+        if signal.dtype != torch.int32 or signal.device != self.dev or logprobs.dtype != torch.float32 \
+                or logprobs.device != self.dev:
+            raise ValueError("signal int32 and logprobs fp32 on the session's device")
+        if not 0 < b <= self.max_batch:
+            raise ValueError(f"batch {b} outside 1..{self.max_batch}")
+        self._check_ring_args(b, slab, rings, ring_ids, rows_in, rows_out)
+        if signal.dim() < 2 or signal.shape[1] != self.chunk_samples or not signal.is_contiguous():
+            raise ValueError(f"signal must be a contiguous (B, {self.chunk_samples}) int32 tensor")
+        if not logprobs.is_contiguous() or logprobs.numel() < b * self.frames * C.VOCAB:
+            raise ValueError("logprobs must be contiguous with room for (B, frames, 35)")
+        if check:
+            both = torch.cat([rows_in, rows_out])
+            if int(both.min()) < 0 or int(both.max()) >= slab.shape[0] or int(torch.unique(both).numel()) != 2 * b:
+                raise ValueError("row ids must be distinct and in range: no row both read and written")
+            if int(ring_ids.min()) < 0 or int(ring_ids.max()) >= rings.shape[0] or int(torch.unique(ring_ids).numel()) != b:
+                raise ValueError(f"ring ids must be distinct and in [0, {rings.shape[0]})")
+        st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
+        _lib.check(self._lib.tone_session_run_ring(self._h, signal.data_ptr(), rows_in.data_ptr(), rows_out.data_ptr(),
+                                                   slab.data_ptr(), slab.stride(0), rings.data_ptr(), ring_ids.data_ptr(),
+                                                   logprobs.data_ptr(), b, st), "tone_session_run_ring")
+
+    def ring_import(self, flat, slab, rows, rings, ring_ids, stream=None) -> None:
+        """Flat states (n, >= 219729) fp16 -> slab rows ``rows`` + rings ``ring_ids`` (chunk counter 0)."""
+        torch = _torch()
+        n = int(flat.shape[0])
+        if flat.dtype != torch.float16 or flat.device != self.dev or flat.dim() != 2 or flat.stride(1) != 1 \
+                or flat.shape[1] < C.STATE_SIZE:
+            raise ValueError("flat must be (n, >= 219729) fp16 on the session's device")
+        self._check_ring_args(n, slab, rings, ring_ids, rows)
+        st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
+        _lib.check(self._lib.tone_session_ring_import(self._h, flat.data_ptr(), flat.stride(0), slab.data_ptr(),
+                                                      slab.stride(0), rows.data_ptr(), rings.data_ptr(),
+                                                      ring_ids.data_ptr(), n, st), "tone_session_ring_import")
+
+    def ring_export(self, slab, rows, rings, ring_ids, flat=None, stream=None):
+        """Slab rows ``rows`` + rings ``ring_ids`` -> flat states (n, 219729) fp16 (allocated when ``flat`` is None)."""
+        torch = _torch()
+        n = int(rows.shape[0])
+        if flat is None:
+            flat = torch.empty((n, C.STATE_SIZE), dtype=torch.float16, device=self.dev)
+        if flat.dtype != torch.float16 or flat.device != self.dev or flat.dim() != 2 or flat.stride(1) != 1 \
+                or flat.shape[0] != n or flat.shape[1] < C.STATE_SIZE:
+            raise ValueError(f"flat must be ({n}, >= 219729) fp16 on the session's device")
+        self._check_ring_args(n, slab, rings, ring_ids, rows)
+        st = (stream or torch.cuda.current_stream(self.dev)).cuda_stream
+        _lib.check(self._lib.tone_session_ring_export(self._h, slab.data_ptr(), slab.stride(0), rows.data_ptr(),
+                                                      rings.data_ptr(), ring_ids.data_ptr(), flat.data_ptr(),
+                                                      flat.stride(0), n, st), "tone_session_ring_export")
+        return flat
+
     def set_frame_info(self, frame_info=None) -> None:
         """Have later runs also write frame_info int32 (>= max_batch, 10): greedy token | speech << 8
         (include/tonehip.h); None switches it off."""

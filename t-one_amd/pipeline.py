@@ -15,9 +15,10 @@ and the splitter / greedy decoder below run on (token, speech) frames with the r
   * phrase times            pipeline.py:151-168
 
 ``StreamingGreedyPipeline`` serves many concurrent streams from one ``ToneSession``: each stream owns
-two rows of a device-resident state slab used in ping-pong, every step runs the streams that have
-audio as one batch through ``tone_session_run_rows`` (read one row, write the other; streams without
-audio are not touched, no state is copied), and only the frame info crosses PCIe.
+two rows of a device-resident state slab used in ping-pong and (resident form, the default) one conv-cache
+ring updated in place, every step runs the streams that have audio as one batch through
+``tone_session_run_ring`` (``tone_session_run_rows`` with ``resident=False``: read one row, write the other;
+streams without audio are not touched, no state is copied), and only the frame info crosses PCIe.
 ``StreamScheduler`` puts an arrival queue in front of it (the role Triton's dynamic / sequence
 batcher plays for the reference, configs/streaming_acoustic/config.pbtxt:35-37,
 triton/model/config.pbtxt:26-69): chunks arrive per stream at any time, each step packs up to
@@ -132,7 +133,9 @@ class StreamingGreedyPipeline:
     state slab, ``forward`` advances any subset of open streams by one 300 ms chunk each.
 
     Slot s owns slab rows 2s and 2s+1; ``_parity[s]`` says which one holds its current state.  A
-    step reads row 2s + p and writes row 2s + 1 - p for the stepping streams only.
+    step reads row 2s + p and writes row 2s + 1 - p for the stepping streams only.  With ``resident`` (default)
+    slot s also owns conv ring s (include/tonehip.h tone_session_run_ring: the conv caches, 84 % of the state,
+    updated in place -- only the step's new frames are written); ``state_of`` then exports the flat state.
 
     ``decoder``: optional host decoder with the reference's ``forward(logprobs (L, 35) float32) -> str``
     (``tone.decoder.BeamSearchCTCDecoder`` -- pyctcdecode + KenLM, BASELINE config 5 -- or
@@ -144,7 +147,7 @@ class StreamingGreedyPipeline:
 
     CHUNK_SIZE = C.AUDIO_CHUNK_SAMPLES   # 300 ms; a session built with chunk_samples=3200 serves 400 ms chunks
 
-    def __init__(self, session, n_slots: int, decoder=None):
+    def __init__(self, session, n_slots: int, decoder=None, resident: bool = True):
         import torch
         if n_slots <= 0:
             raise ValueError("n_slots must be positive")
@@ -154,6 +157,9 @@ class StreamingGreedyPipeline:
         self.frames = fr = int(getattr(session, "frames", C.CHUNK_FRAMES))
         dev = session.dev
         self._slab = torch.zeros((2 * self.n_slots, STATE_STRIDE), dtype=torch.float16, device=dev)
+        self.resident = bool(resident)
+        self._rings = torch.zeros((self.n_slots, session.ring_elems), dtype=torch.float16, device=dev) \
+            if self.resident else None
         self._parity = np.zeros(self.n_slots, np.int32)
         self._open: dict[int, FrameSplitterState] = {}
         self._free = list(range(self.n_slots - 1, -1, -1))
@@ -162,9 +168,9 @@ class StreamingGreedyPipeline:
         self._info = torch.zeros((mb, fr), dtype=torch.int32, device=dev)
         self._logp = torch.empty((mb, fr, C.VOCAB), dtype=torch.float32, device=dev)
         self._sig = torch.zeros((mb, self.CHUNK_SIZE), dtype=torch.int32, device=dev)
-        self._rows = torch.zeros((2, mb), dtype=torch.int32, device=dev)
+        self._rows = torch.zeros((3, mb), dtype=torch.int32, device=dev)   # rows read / written, ring ids
         self._sig_h = torch.zeros((mb, self.CHUNK_SIZE), dtype=torch.int32).pin_memory()
-        self._rows_h = torch.zeros((2, mb), dtype=torch.int32).pin_memory()
+        self._rows_h = torch.zeros((3, mb), dtype=torch.int32).pin_memory()
         self._info_h = torch.zeros((mb, fr), dtype=torch.int32).pin_memory()
         self.decoder = decoder
         self._logp_h = torch.zeros((mb, fr, C.VOCAB), dtype=torch.float32).pin_memory() \
@@ -183,6 +189,8 @@ class StreamingGreedyPipeline:
         slot = self._free.pop()
         self._parity[slot] = 0
         self._slab[2 * slot].zero_()          # onnx_wrapper.py:114-115: zero state at stream start
+        if self.resident:
+            self._rings[slot].zero_()         # (the zero row's conv section holds chunk counter 0)
         self._open[slot] = self._fresh_state()
         return slot
 
@@ -197,10 +205,17 @@ class StreamingGreedyPipeline:
         return sorted(self._open)
 
     def state_of(self, slot: int):
-        """The current flat (219729,) fp16 state of an open stream (a device tensor view)."""
+        """The current flat (219729,) fp16 state of an open stream: a view of its slab row, or with the resident
+        form the row and ring exported to a new device tensor."""
+        import torch
         if slot not in self._open:
             raise KeyError(f"slot {slot} is not open")
-        return self._slab[2 * slot + int(self._parity[slot]), : C.STATE_SIZE]
+        row = 2 * slot + int(self._parity[slot])
+        if not self.resident:
+            return self._slab[row, : C.STATE_SIZE]
+        dev = self.session.dev
+        ids = torch.tensor([row, slot], dtype=torch.int32, device=dev)
+        return self.session.ring_export(self._slab, ids[:1], self._rings, ids[1:])[0]
 
     # --- one step ----------------------------------------------------------------------------
     def step_frames(self, chunks: np.ndarray, slots: Sequence[int]) -> np.ndarray:
@@ -219,10 +234,16 @@ class StreamingGreedyPipeline:
             self._sig_h[:nb].numpy()[:] = chunks[b0:b1]
             self._rows_h[0, :nb].numpy()[:] = 2 * sl + par
             self._rows_h[1, :nb].numpy()[:] = 2 * sl + 1 - par
+            self._rows_h[2, :nb].numpy()[:] = sl
             self._sig[:nb].copy_(self._sig_h[:nb], non_blocking=True)
             self._rows[:, :nb].copy_(self._rows_h[:, :nb], non_blocking=True)
-            self.session.run_rows(self._sig[:nb], self._rows[0, :nb], self._rows[1, :nb], self._slab,
-                                  self._logp, check_rows=False)   # rows are built here, distinct by construction
+            # rows and ring ids are built here, distinct by construction
+            if self.resident:
+                self.session.run_ring(self._sig[:nb], self._rows[0, :nb], self._rows[1, :nb], self._slab, self._rings,
+                                      self._rows[2, :nb], self._logp, check=False)
+            else:
+                self.session.run_rows(self._sig[:nb], self._rows[0, :nb], self._rows[1, :nb], self._slab,
+                                      self._logp, check_rows=False)
             self._info_h[:nb].copy_(self._info[:nb], non_blocking=True)
             if logp is not None:
                 self._logp_h[:nb].copy_(self._logp[:nb], non_blocking=True)

@@ -260,13 +260,15 @@ def oracle():
 
 
 @pytest.mark.gpu
-def test_ping_pong_rows_vs_oracle(session, oracle):
+@pytest.mark.parametrize("resident", [True, False])
+def test_ping_pong_rows_vs_oracle(session, oracle, resident):
     """Streams that join late and sit idle for several steps (their rows untouched, no state copy):
     every stepping stream's logprobs vs the oracle stepped from that stream's device state, <= 1e-3;
-    idle streams' states bit-identical across the steps they skip."""
+    idle streams' states bit-identical across the steps they skip.  Both state forms: resident (conv caches in
+    rings, run_ring; state_of exports) and flat ping-pong rows (run_rows)."""
     import torch
     rng = np.random.default_rng(19)
-    pipe = P.StreamingGreedyPipeline(session, n_slots=6)
+    pipe = P.StreamingGreedyPipeline(session, n_slots=6, resident=resident)
     try:
         sched = [["A"], ["A", "B"], ["B", "C", "D"], ["A", "D"], ["A", "B", "C", "D"], ["C"], ["A", "B", "C", "D"]]
         slot = {}

@@ -227,6 +227,18 @@ def test_dwconv_every_element(B, T, check, tol):
     _state_ok(r, 0)
 
 
+@pytest.mark.parametrize("B,T,check,tol", [(4096, 10, "dwconv_ring_bf16", 1e-2), (4096, 5, "dwconv_ring_bf16", 1e-2),
+                                            (2048, 13, "dwconv_ring_bf16", 1e-2), (2048, 6, "dwconv_ring_bf16", 1e-2),
+                                            (256, 10, "dwconv_ring", 1e-5), (256, 5, "dwconv_ring", 1e-5),
+                                            (1, 10, "dwconv_ring", 1e-5)])
+def test_dwconv_ring_every_element(B, T, check, tol):
+    """The resident-form depthwise conv (cache frame i at ring row (n T + i) mod 30, the T new frames written over the T
+    oldest): output, and every byte of every ring (the other rows, layers and the unused ring unchanged)."""
+    _gpu()
+    r = _check(check, B, T)
+    assert r["outputs"]["out"] < tol and r["outputs"]["ring_bad_bytes"] == 0, r
+
+
 REC_TS = [(10, 0), (5, 0), (5, 15), (10, 30), (13, 0), (6, 0), (6, 15), (13, 30)]
 
 
