@@ -414,6 +414,9 @@ int main(int argc, char** argv) {
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
     a.res16 = res16 && !f32;
+    // the residual buffer in the type the variant reads: an fp32 variant under RES16 must not be handed the fp16
+    // buffer (half the bytes: it read past the end -- a GPU memory fault, round 6)
+    a.R = a.res16 ? reinterpret_cast<const float*>(R16) : R;
     a.norm_w = (v >= 90 && v <= 98) ? normw : nullptr;
     // HBLK=1: gemm_xw SWIGLU writes / gemm_rp reads the blocked hidden (checked through a row-major copy / built from one)
     const bool hblk = getenv("HBLK") && atoi(getenv("HBLK")) && ((vv <= -300 && epi == 2) || (v >= 90 && v <= 98 && epi == 1));
