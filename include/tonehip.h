@@ -119,13 +119,15 @@ int tone_session_run_slots(tone_session *s, const int32_t *signal, const int32_t
 int tone_session_run_rows(tone_session *s, const int32_t *signal, const int32_t *rows_in, const int32_t *rows_out,
                           uint16_t *slab, int64_t slab_stride, float *logprobs, int batch, void *stream);
 
-/* Same step with the state in its RESIDENT form: the conv-module caches (the (16, 384, 30) section, 84 % of the
- * 439 KB state) live outside the rows in one ring per stream, updated in place -- a step reads the 30 cached frames
- * and writes only its T new ones over the T oldest, where the flat form rewrites the whole window shifted by T.
+/* Same step with the state in its RESIDENT form: the conv-module caches and the layer 14 / 15 MHSA input caches (the
+ * (16, 384, 30) and (2, 30, 384) sections, 94 % of the 439 KB state) live outside the rows in one ring per stream,
+ * updated in place -- a step reads the cached frames and writes only its T new ones over the T oldest, where the flat
+ * form rewrites the whole window shifted by T.
  *   rows_in/out int32 [batch]                     ping-pong rows of `slab` for the other sections (as run_rows)
- *   rings       fp16  [n_rings][tone_session_ring_elems()]   time-major [16][30][384]
+ *   rings       fp16  [n_rings][tone_session_ring_elems()]   time-major [16 + 2][30][384]
  *   ring_ids    int32 [batch]                     stream i's ring (distinct, in [0, n_rings), unchecked)
- * The row's conv section then holds only the stream's chunk counter (mod 30), which sets the rings' phases.
+ * The row's conv section then holds only the stream's chunk counter (mod 30), which sets the rings' phases; its mhsa
+ * section is unused.
  * Results (logprobs, and the state once exported) are bit-identical to the flat form's.  Convert with
  * tone_session_ring_import (flat row i -> slab row rows[i] + ring ring_ids[i]; a zero flat state gives a fresh stream)
  * and tone_session_ring_export (the inverse: the flat (B, 219729) state at the boundary). */
@@ -138,7 +140,7 @@ int tone_session_ring_import(tone_session *s, const uint16_t *flat, int64_t flat
 int tone_session_ring_export(tone_session *s, const uint16_t *slab, int64_t slab_stride, const int32_t *rows,
                              const uint16_t *rings, const int32_t *ring_ids, uint16_t *flat, int64_t flat_stride, int n,
                              void *stream);
-/* fp16 elements of one stream's ring (16 x 30 x 384). */
+/* fp16 elements of one stream's ring ((16 + 2) x 30 x 384). */
 int64_t tone_session_ring_elems(void);
 
 /* Workspace bytes the session holds on the device (weights + activations). */

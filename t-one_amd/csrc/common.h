@@ -87,12 +87,16 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // Where stream b's state rows live: row b of state_in / state_out, or rows slots[b] of device-resident
 // slabs; with slots_out, stream b reads row slots[b] and writes row slots_out[b] (ping-pong rows of one
 // slab, so streams that sit out a step keep their state without a copy).
-// Resident (ring) form, tone_session_run_ring: the conv-module caches of stream b live outside its row, in the ring
-// ring + ring_ids[b] * kRingElems, time-major [16 layers][30 frames][384 channels] fp16, updated in place: a step writes
-// only its T new frames, over the T oldest (the flat form rewrites all 30 shifted by T).  Cache frame i of layer l sits
-// at ring row (ph_l + i) mod 30, ph_l = (n T_l) mod 30, n = the stream's chunk counter mod 30, kept (as fp16) at the
-// first element of the row's then unused conv section; T_l = the layer's frames per step (T, or Tr in layers 7-14).
-constexpr int64_t kRingElems = (int64_t)16 * 30 * 384;   // 184320 = the flat conv section's size
+// Resident (ring) form, tone_session_run_ring: the conv-module caches and the layer 14 / 15 MHSA input caches of stream b
+// live outside its row, in the ring ring + ring_ids[b] * kRingElems, time-major [16 conv layers + 2 MHSA layers][30
+// frames][384 channels] fp16, updated in place: a step writes only its T new frames, over the T oldest (the flat form
+// rewrites all 30 shifted by T).  Cache frame i of layer l sits at ring row (ph_l + i) mod 30, ph_l = (n T_l) mod 30,
+// n = the stream's chunk counter mod 30, kept (as fp16) at the first element of the row's then unused conv section;
+// T_l = the layer's frames per step (T, or Tr in layers 7-14).  The MHSA caches' frames older than the layer's S
+// (layer 14: S = 15) are the flat form's zero padding: stale in the ring, zeros on export.
+constexpr int64_t kRingConv = (int64_t)16 * 30 * 384;    // 184320 = the flat conv section's size
+constexpr int64_t kRingMhsa = (int64_t)2 * 30 * 384;     // 23040 = the flat mhsa section's size
+constexpr int64_t kRingElems = kRingConv + kRingMhsa;
 __host__ __device__ __forceinline__ int ring_phase(int n, int T) { return (n * T) % 30; }
 
 struct StateRef {

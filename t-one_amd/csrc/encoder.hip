@@ -71,6 +71,27 @@ hipError_t launch_rmsnorm(void* x, const float* w, int rows, uint16_t* shadow, i
 // to its last S rows (conformer_blocks.py:147-148); MultiHeadAttention.update_state attends over
 // kv = [cache_S ; xn] and keeps [cache_S[T:] ; xn] (submodules.py:295-302); update_after_layer
 // left-pads it with zeros to 30 rows (conformer_blocks.py:161-163).  xn = norm_self_att(r).
+// norm_self_att of one residual row held by a wave (6 values per lane): ss by an explicit fma chain, den = fma(sqrt(ss),
+// 1/sqrt(384), eps), y = w (v / den) rounded to fp32 -- with contraction off, so that the flat and the resident kernels
+// (and every store of y: fp32 / bf16 activations, the fp16 cache) see the same bits whatever the compiler fuses around
+// them (left to itself it summed ss with an fma chain in one kernel and with paired products in the other, and fused
+// the product into the fp16 conversion as a v_fma_mixlo for some rows only).
+template <bool OBF>
+__device__ __forceinline__ void mhsa_norm_row(const void* __restrict__ r, int64_t xr, const float* __restrict__ norm_w,
+                                              int lane, float (&y)[6]) {
+#pragma clang fp contract(off)
+  float v[6], ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 6; ++e) { v[e] = load_res<OBF>(r, xr + lane + 64 * e); ss = fmaf(v[e], v[e], ss); }
+  ss = wave_sum(ss);
+  const float den = fmaf(sqrtf(ss), kInvSqrtD, kRmsEps);
+#pragma unroll
+  for (int e = 0; e < 6; ++e) {
+    y[e] = norm_w[lane + 64 * e] * (v[e] / den);
+    asm("" : "+v"(y[e]));   // y is an fp32 value from here on: no fusing the product into a later conversion
+  }
+}
+
 template <bool OBF>
 __global__ void __launch_bounds__(256) kv_assemble_kernel(const void* __restrict__ r, const float* __restrict__ norm_w,
                                                           StateRef s, int layer_slot, int T, int S,
@@ -85,15 +106,12 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const void* __restrict
   // normalized current rows
   for (int i = 4 * y + wid; i < T; i += 4 * ns) {
     const int64_t xr = ((int64_t)b * T + i) * kD;   // the residual stream: fp16 in the bf16 / fp8 modes (OBF)
-    float v[6], ss = 0.f;
-#pragma unroll
-    for (int e = 0; e < 6; ++e) { v[e] = load_res<OBF>(r, xr + lane + 64 * e); ss += v[e] * v[e]; }
-    ss = wave_sum(ss);
-    const float den = sqrtf(ss) * kInvSqrtD + kRmsEps;
+    float v[6];
+    mhsa_norm_row<OBF>(r, xr, norm_w, lane, v);
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
       const int c = lane + 64 * e;
-      const float y = norm_w[c] * (v[e] / den);
+      const float y = v[e];
       store_act<OBF>(xn, ((int64_t)b * T + i) * kD + c, y);
       store_act<OBF>(kv, ((int64_t)b * TK + S + i) * kD + c, y);
       // new cache row (30 - S) + (S - T + i) = 30 - T + i holds xn[i]
@@ -114,8 +132,58 @@ __global__ void __launch_bounds__(256) kv_assemble_kernel(const void* __restrict
   }
 }
 
+// The same on the resident form (common.h StateRef): the layer's 30 cached frames in the stream's ring (frame i at row
+// (ph + i) mod 30), one workgroup per stream.  kv's cached rows are the ring's frames 30 - S .. 29; after a workgroup
+// barrier (those reads done) the T new xn rows go over the T oldest ring rows ph .. ph + T - 1 -- no rewrite of the
+// S - T kept rows or of layer 14's zero padding.  Same arithmetic as kv_assemble_kernel.
+template <bool OBF>
+__global__ void __launch_bounds__(256) kv_assemble_ring_kernel(const void* __restrict__ r, const float* __restrict__ norm_w,
+                                                               StateRef s, int layer_slot, int T, int S,
+                                                               void* __restrict__ xn, void* __restrict__ kv) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ph = ring_phase(s.chunk_counter(b), T);
+  __half* rg = s.ring + (int64_t)s.ring_ids[b] * kRingElems + kRingConv + (int64_t)layer_slot * kMhsaS * kD;
+  const int TK = S + T;
+  constexpr int kMaxRowsPerWave = (kTMax + 3) / 4;
+  float y[kMaxRowsPerWave][6];
+  // normalized current rows (wave w: rows w, w + 4, ...)
+#pragma unroll
+  for (int q = 0; q < kMaxRowsPerWave; ++q) {
+    const int i = wid + 4 * q;
+    if (i >= T) break;
+    const int64_t xr = ((int64_t)b * T + i) * kD;
+    mhsa_norm_row<OBF>(r, xr, norm_w, lane, y[q]);
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const int c = lane + 64 * e;
+      store_act<OBF>(xn, ((int64_t)b * T + i) * kD + c, y[q][e]);
+      store_act<OBF>(kv, ((int64_t)b * TK + S + i) * kD + c, y[q][e]);
+    }
+  }
+  // cached rows: ring frames 30 - S .. 29
+  for (int i = tid; i < S * kD; i += 256) {
+    const int j = i / kD, c = i % kD;
+    const int fr = ph + kMhsaS - S + j;
+    store_act<OBF>(kv, ((int64_t)b * TK + j) * kD + c, __half2float(rg[(int64_t)(fr % kMhsaS) * kD + c]));
+  }
+  __syncthreads();   // every ring read of this stream is done before its oldest rows are overwritten
+#pragma unroll
+  for (int q = 0; q < kMaxRowsPerWave; ++q) {
+    const int i = wid + 4 * q;
+    if (i >= T) break;
+    const int row = ph + i < kMhsaS ? ph + i : ph + i - kMhsaS;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) rg[(int64_t)row * kD + lane + 64 * e] = __float2half_rn(y[q][e]);
+  }
+}
+
 hipError_t launch_kv_assemble(const void* r, const float* norm_w, StateRef s, int layer_slot, int T, int S, void* xn,
                               void* kv, bool obf, int B, hipStream_t st) {
+  if (s.ring) {
+    if (obf) hipLaunchKernelGGL(kv_assemble_ring_kernel<true>, dim3(B), dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
+    else hipLaunchKernelGGL(kv_assemble_ring_kernel<false>, dim3(B), dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
+    return hipGetLastError();
+  }
   const dim3 grid(B, B >= 1024 ? 1 : 4);
   if (obf) hipLaunchKernelGGL(kv_assemble_kernel<true>, grid, dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
   else hipLaunchKernelGGL(kv_assemble_kernel<false>, grid, dim3(256), 0, st, r, norm_w, s, layer_slot, T, S, xn, kv);
@@ -756,15 +824,18 @@ __global__ void __launch_bounds__(256) ring_import_kernel(const __half* __restri
   const __half* f = flat + (int64_t)i * fstride;
   __half* r = slab + (int64_t)rows[i] * sstride;
   __half* rg = ring + (int64_t)ring_ids[i] * kRingElems;
+  // every section but conv and mhsa (the ring's); the conv section's first element = chunk counter 0
   for (int64_t e = threadIdx.x; e < kStateSize; e += 256) {
-    if (e < kOffConv || e >= kOffConv + kRingElems) r[e] = f[e];
+    const bool conv = e >= kOffConv && e < kOffConv + kRingConv, mhsa = e >= kOffMhsa && e < kOffMhsa + kRingMhsa;
+    if (!conv && !mhsa) r[e] = f[e];
     else if (e == kOffConv) r[e] = __float2half_rn(0.f);
   }
-  // ring[l][t][c] = flat conv[l][c][t]
-  for (int64_t e = threadIdx.x; e < kRingElems; e += 256) {
+  // conv: ring[l][t][c] = flat conv[l][c][t]; mhsa: ring[16 + ls][t][c] = flat mhsa[ls][t][c] (both time-major there)
+  for (int64_t e = threadIdx.x; e < kRingConv; e += 256) {
     const int c = (int)(e % kD), t = (int)((e / kD) % kConvS), l = (int)(e / (kD * kConvS));
     rg[e] = f[kOffConv + ((int64_t)l * kD + c) * kConvS + t];
   }
+  for (int64_t e = threadIdx.x; e < kRingMhsa; e += 256) rg[kRingConv + e] = f[kOffMhsa + e];
 }
 
 __global__ void __launch_bounds__(256) ring_export_kernel(const __half* __restrict__ slab, int64_t sstride,
@@ -776,13 +847,23 @@ __global__ void __launch_bounds__(256) ring_export_kernel(const __half* __restri
   __half* f = flat + (int64_t)i * fstride;
   const __half* rg = ring + (int64_t)ring_ids[i] * kRingElems;
   const int n = (int)__half2float(r[kOffConv]);
-  for (int64_t e = threadIdx.x; e < kStateSize; e += 256)
-    if (e < kOffConv || e >= kOffConv + kRingElems) f[e] = r[e];
+  for (int64_t e = threadIdx.x; e < kStateSize; e += 256) {
+    const bool conv = e >= kOffConv && e < kOffConv + kRingConv, mhsa = e >= kOffMhsa && e < kOffMhsa + kRingMhsa;
+    if (!conv && !mhsa) f[e] = r[e];
+  }
   // flat conv[l][c][t] = ring[l][(ph_l + t) mod 30][c]
-  for (int64_t e = threadIdx.x; e < kRingElems; e += 256) {
+  for (int64_t e = threadIdx.x; e < kRingConv; e += 256) {
     const int t = (int)(e % kConvS), c = (int)((e / kConvS) % kD), l = (int)(e / (kD * kConvS));
     const int ph = ring_phase(n, (l > 6 && l <= 14) ? Tr : T);
     f[kOffConv + e] = rg[((int64_t)l * kConvS + (ph + t) % kConvS) * kD + c];
+  }
+  // flat mhsa[ls][t][c] = ring[16 + ls][(ph + t) mod 30][c] for the layer's last S frames, zero below (the flat form's
+  // left padding: layer 14 (ls 0) in the reduced block, S = 15, T_l = Tr; layer 15, S = 30, T_l = T)
+  for (int64_t e = threadIdx.x; e < kRingMhsa; e += 256) {
+    const int c = (int)(e % kD), t = (int)((e / kD) % kMhsaS), ls = (int)(e / (kD * kMhsaS));
+    const int S = ls == 0 ? kMhsaS / 2 : kMhsaS, ph = ring_phase(n, ls == 0 ? Tr : T);
+    f[kOffMhsa + e] = t < kMhsaS - S ? __float2half_rn(0.f)
+                                     : rg[kRingConv + ((int64_t)ls * kMhsaS + (ph + t) % kMhsaS) * kD + c];
   }
 }
 

@@ -823,6 +823,84 @@ __global__ void ref_kv_kernel(const void* r, int rty, const float* nw, StateRef 
   }
 }
 
+// the resident form: cache frame j at ring row (n_b T + j) mod 30 of ring region 16 + slot; expected ring = the T new xn
+// rows over rows (n_b T + i) mod 30 (counter n_b = (7 b + 3) mod 30 as set_counter_kernel writes it)
+__global__ void ref_kv_ring_kernel(const void* r, int rty, const float* nw, StateRef s, const __half* ring0, int slot, int T,
+                                   int S, float* xn, float* kv, __half* ring_exp, int B) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * kD) return;
+  const int b = (int)(i / kD), c = (int)(i % kD);
+  const int TK = S + T, n = (7 * b + 3) % kMhsaS, ph = (n * T) % kMhsaS;
+  const int64_t base = (int64_t)s.ring_ids[b] * kRingElems + kRingConv + (int64_t)slot * kMhsaS * kD + c;
+  for (int t = 0; t < T; ++t) {
+    double ss = 0.0;
+    for (int k = 0; k < kD; ++k) {
+      const double v = load_typed(r, rty, ((int64_t)b * T + t) * kD + k);
+      ss += v * v;
+    }
+    const double den = sqrt(ss) / sqrt((double)kD) + 1e-8;
+    const float y = (float)((double)nw[c] * ((double)load_typed(r, rty, ((int64_t)b * T + t) * kD + c) / den));
+    xn[((int64_t)b * T + t) * kD + c] = y;
+    kv[((int64_t)b * TK + S + t) * kD + c] = y;
+    ring_exp[base + (int64_t)((ph + t) % kMhsaS) * kD] = __float2half_rn(y);
+  }
+  for (int j = 0; j < S; ++j)
+    kv[((int64_t)b * TK + j) * kD + c] = h2f(ring0[base + (int64_t)((ph + kMhsaS - S + j) % kMhsaS) * kD]);
+}
+
+__global__ void set_counter_kernel(StateRef s, int B);
+__global__ void cmp_bytes_kernel(const uint8_t* a, const uint8_t* b, int64_t n, int* bad);
+// fp16 ulp distance of two fp16 buffers, max over elements (the recomputed xn rows of the ring)
+__global__ void ulp_kernel(const __half* a, const __half* b, int64_t n, int* mx) {
+  int d = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint16_t x = __half_as_ushort(a[i]), y = __half_as_ushort(b[i]);
+    const int ox = (x & 0x8000) ? -(int)(x & 0x7fff) : (int)x, oy = (y & 0x8000) ? -(int)(y & 0x7fff) : (int)y;
+    d = max(d, abs(ox - oy));
+  }
+  if (d) atomicMax(mx, d);
+}
+
+static void check_kv_ring(int B, int T, int S, bool bf, Report& rep) {
+  Slab sl;
+  sl.make(B);
+  const int slot = S == 15 ? 0 : 1, TK = S + T, nr = B + 1;
+  std::vector<int> ids(B);
+  for (int b = 0; b < B; ++b) ids[b] = (int)(((int64_t)5 * b + 1) % nr);
+  int* dids = pool.get<int>(B);
+  CK(hipMemcpy(dids, ids.data(), B * 4, hipMemcpyHostToDevice));
+  StateRef sr = sl.ref();
+  sr.ring = to_f16(rand_f32((int64_t)nr * kRingElems, 35, 2.f), (int64_t)nr * kRingElems);
+  sr.ring_ids = dids;
+  hipLaunchKernelGGL(set_counter_kernel, grid1(B), dim3(256), 0, 0, sr, B);
+  __half* ring0 = pool.get<__half>((int64_t)nr * kRingElems);
+  __half* ring_exp = pool.get<__half>((int64_t)nr * kRingElems);
+  CK(hipMemcpy(ring0, sr.ring, (size_t)nr * kRingElems * 2, hipMemcpyDeviceToDevice));
+  CK(hipMemcpy(ring_exp, sr.ring, (size_t)nr * kRingElems * 2, hipMemcpyDeviceToDevice));
+  const int64_t M = (int64_t)B * T;
+  float* rf = rand_f32(M * kD, 51, 3.f);
+  const void* r = bf ? (const void*)to_f16(rf, M * kD) : (const void*)rf;
+  const float* nw = rand_f32(kD, 52, 0.2f, 1.f);
+  void* xn = bf ? (void*)pool.get<uint16_t>(M * kD) : (void*)pool.get<float>(M * kD);
+  void* kv = bf ? (void*)pool.get<uint16_t>((int64_t)B * TK * kD) : (void*)pool.get<float>((int64_t)B * TK * kD);
+  float* xr = pool.get<float>(M * kD);
+  float* kr = pool.get<float>((int64_t)B * TK * kD);
+  hipLaunchKernelGGL(ref_kv_ring_kernel, grid1((int64_t)B * kD), dim3(256), 0, 0, r, bf ? 2 : 0, nw, sr, ring0, slot, T, S, xr,
+                     kr, ring_exp, B);
+  CK(hipDeviceSynchronize());
+  rep.us = time_once([=] { return launch_kv_assemble(r, nw, sr, slot, T, S, xn, kv, bf, B, 0); });
+  rep.out("xn", xn, bf ? 1 : 0, kD, xr, M, kD);
+  rep.out("kv", kv, bf ? 1 : 0, kD, kr, (int64_t)B * TK, kD);
+  // every ring element within one fp16 ulp of the expected rings (copies exact, the new xn rows one rounding of a
+  // value computed in another order), the rest of every ring (conv layers, the other MHSA layer) byte-exact
+  int* mx = pool.get<int>(1);
+  CK(hipMemset(mx, 0, 4));
+  hipLaunchKernelGGL(ulp_kernel, dim3(2048), dim3(256), 0, 0, sr.ring, ring_exp, (int64_t)nr * kRingElems, mx);
+  int hm = 0;
+  CK(hipMemcpy(&hm, mx, 4, hipMemcpyDeviceToHost));
+  rep.outs.emplace_back("ring_max_ulp", Res{(float)hm, 0, 0, 0, 0, 0});
+}
+
 static void check_kv(int B, int T, int S, bool bf, Report& rep) {
   Slab sl;
   sl.make(B);
@@ -1087,6 +1165,7 @@ int main(int argc, char** argv) {
   else if (ck.rfind("dwconv", 0) == 0) check_dwconv(B, T, bf, rep);
   else if (ck.rfind("attn_rec", 0) == 0) check_attention(B, T, S, true, bf, rep);
   else if (ck.rfind("attn_shared", 0) == 0) check_attention(B, T, 0, false, bf, rep);
+  else if (ck.rfind("kv_ring", 0) == 0) check_kv_ring(B, T, S, bf, rep);
   else if (ck.rfind("kv", 0) == 0) check_kv(B, T, S, bf, rep);
   else if (ck.rfind("reduce", 0) == 0) check_reduce(B, T, bf, rep);
   else if (ck.rfind("upsample", 0) == 0) check_upsample(B, T, has("_r16"), rep);

@@ -177,7 +177,7 @@ class ToneSession:
     # --- resident state: conv caches in per-stream rings (include/tonehip.h tone_session_run_ring) ----------------
     @property
     def ring_elems(self) -> int:
-        """fp16 elements of one stream's conv ring (16 x 30 x 384)."""
+        """fp16 elements of one stream's ring ((16 conv + 2 MHSA layers) x 30 x 384)."""
         return int(self._lib.tone_session_ring_elems())
 
     def _check_ring_args(self, b, slab, rings, ids, *row_lists):

@@ -274,6 +274,17 @@ def test_kv_assemble_every_element(T, S, check, B, tol):
     _state_ok(r, 1)
 
 
+@pytest.mark.parametrize("T,S", [(5, 15), (10, 30), (6, 15), (13, 30)])
+@pytest.mark.parametrize("check,B,tol", [("kv_ring_bf16", 4096, 1e-2), ("kv_ring", 256, 1e-5), ("kv_ring", 1, 1e-5)])
+def test_kv_assemble_ring_every_element(T, S, check, B, tol):
+    """The resident-form MHSA cache: kv's cached rows from ring frames 30 - S .. 29 (row (n T + j) mod 30), the T new
+    xn rows written over the T oldest ring rows; every element of every ring (conv layers and the other MHSA layer
+    unchanged, the new rows within one fp16 rounding)."""
+    _gpu()
+    r = _check(check, B, T, S)
+    assert r["outputs"]["xn"] < tol and r["outputs"]["kv"] < tol and r["outputs"]["ring_max_ulp"] <= 1, r
+
+
 @pytest.mark.parametrize("T", [10, 13])
 @pytest.mark.parametrize("check,B,tol", [("reduce_bf16", 4096, 1e-2), ("reduce", 256, 1e-5)])
 def test_reduce_conv_every_element(T, check, B, tol):
