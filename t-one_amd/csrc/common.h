@@ -332,6 +332,28 @@ __host__ __device__ __forceinline__ int64_t hblk_off(int64_t row, int col, int64
   return ((row >> 5) * (ld >> 5) + (col >> 5)) * 1024 + (c >> 1) * 512 + ((c & 1) * 32 + (row & 31)) * 8 + (col & 7);
 }
 
+// fp32 split mode: the operands of gemm_d3 (the N = 384 projections at small M) "fragment-packed", so that every one of
+// its 16-byte-per-lane loads reads 1 KiB contiguous.  A [rows][K] fp32 activation (rows padded to a multiple of 32):
+// per 32-row block and 32-column pair block 4 KiB, chunk 2 e + o (e = K-step of the pair, o = which half of the lane's
+// 8 values) holding lane (h, r) = 32 h + r's four values row 32 rb + r, columns 32 p + 16 e + 8 h + 4 o .. + 3 -- the B
+// operand of v_mfma_f32_32x32x16_bf16 for lane 32 h + r once split.  Written by the producers of those A operands
+// (the fp32 SwiGLU epilogue, the attention kernels, the depthwise conv) when the consumer is routed to gemm_d3.
+__host__ __device__ __forceinline__ int64_t xpk_off(int64_t row, int col, int K) {
+  const int k = col & 31;
+  return (((row >> 5) * (K >> 5) + (col >> 5)) * 4 + 2 * (k >> 4) + ((k >> 2) & 1)) * 256 +
+         (((k >> 3) & 1) * 32 + (row & 31)) * 4 + (k & 3);
+}
+// The element offset of an fp32 activation stored row-major (ld K) or packed as above.
+__host__ __device__ __forceinline__ int64_t act_off(int64_t row, int col, int K, bool packed) {
+  return packed ? xpk_off(row, col, K) : row * K + col;
+}
+// W's three bf16 planes [3][N][K] for gemm_d3: per 32-row block and 32-column pair block 6 KiB, chunk 2 plane + e holding
+// lane (h, r)'s 8 values row 32 nb + r, columns 32 p + 16 e + 8 h .. + 7 (the A operand of the same MFMA).
+__host__ __device__ __forceinline__ int64_t wpk_off(int64_t n, int k, int plane, int K) {
+  return ((((n >> 5) * (K >> 5) + (k >> 5)) * 3 + plane) * 2 + ((k >> 4) & 1)) * 512 + (((k >> 3) & 1) * 32 + (n & 31)) * 8 +
+         (k & 7);
+}
+
 // The residual stream: fp32 in fp32 mode, fp16 in the bf16 / fp8 modes (as the reference's exported graph keeps it,
 // tone/scripts/export.py:411).  Element i, and four consecutive elements (16 / 8-byte aligned),
 // with the type fixed at compile time (R16) or chosen per launch (r16, the GEMM epilogues).

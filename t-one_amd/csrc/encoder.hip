@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(256) attention_kernel(AttnArgs a) {
   }
   if (lane < kDk) {
 #pragma unroll
-    for (int i = 0; i < T; ++i) store_act<OBF>(a.ctx, ((int64_t)b * T + i) * kD + c0 + lane, acc[i]);
+    for (int i = 0; i < T; ++i) store_act<OBF>(a.ctx, act_off((int64_t)b * T + i, c0 + lane, kD, !OBF && a.ctx_packed), acc[i]);
   }
 }
 
@@ -400,7 +400,8 @@ __global__ void __launch_bounds__(256) attention_rec_kernel(AttnArgs a) {
     const int iq = 4 * g + rr;
     if (iq < T) {
 #pragma unroll
-      for (int ct = 0; ct < 3; ++ct) store_act<OBF>(a.ctx, ((int64_t)b * T + iq) * kD + c0 + 16 * ct + r16, cx[ct][rr]);
+      for (int ct = 0; ct < 3; ++ct)
+        store_act<OBF>(a.ctx, act_off((int64_t)b * T + iq, c0 + 16 * ct + r16, kD, !OBF && a.ctx_packed), cx[ct][rr]);
     }
   }
 }
@@ -429,6 +430,7 @@ static hipError_t launch_attention_t(const AttnArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
+  if (a.ctx_bf16 && a.ctx_packed) return hipErrorInvalidValue;   // the packed layout is fp32 (gemm_d3's A)
   return a.ctx_bf16 ? launch_attention_t<true>(a, st) : launch_attention_t<false>(a, st);
 }
 
@@ -447,7 +449,7 @@ constexpr int kDwSec = kD * kConvS;          // 11520 halves per (stream, layer)
 template <int T, bool OBF, int CPW, int NS>
 __global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g, StateRef s, int layer,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
-                                                     void* __restrict__ out, int B) {
+                                                     void* __restrict__ out, int B, int opk) {
   constexpr int kSec = CPW * kConvS;           // halves of this workgroup's slice
   constexpr int kVec = kSec / 8 + 1;           // 16-byte vectors covering a misaligned slice
   __shared__ uint4 lds[NS][kVec];
@@ -497,7 +499,7 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g,
       float y;
       if constexpr (OBF) y = acc * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc * -1.4426950408889634f));
       else y = silu_f(acc);
-      store_act<OBF>(out, ((int64_t)b * T + t) * kD + ch, y);
+      store_act<OBF>(out, act_off((int64_t)b * T + t, ch, kD, !OBF && opk), y);
     }
 #pragma unroll
     for (int i = 0; i < kConvS; ++i) h[i] = __float2half_rn(x[T + i]);
@@ -537,7 +539,7 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g,
 template <int T, bool OBF>
 __global__ void __launch_bounds__(kD / 2) dwconv_ring_kernel(const void* __restrict__ g, StateRef s, int layer,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
-                                                            void* __restrict__ out) {
+                                                            void* __restrict__ out, int opk) {
   const int b = blockIdx.x, c = 2 * threadIdx.x;
   const int ph = ring_phase(s.chunk_counter(b), T);
   __half* rg = s.ring + (int64_t)s.ring_ids[b] * kRingElems + (int64_t)layer * kConvS * kD + c;
@@ -574,7 +576,7 @@ __global__ void __launch_bounds__(kD / 2) dwconv_ring_kernel(const void* __restr
       if constexpr (OBF) y[e] = acc * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc * -1.4426950408889634f));
       else y[e] = silu_f(acc);
     }
-    const int64_t oi = ((int64_t)b * T + t) * kD + c;
+    const int64_t oi = act_off((int64_t)b * T + t, c, kD, !OBF && opk);   // c even: c, c + 1 adjacent packed too
     store_act<OBF>(out, oi, y[0]);
     store_act<OBF>(out, oi + 1, y[1]);
   }
@@ -588,30 +590,33 @@ __global__ void __launch_bounds__(kD / 2) dwconv_ring_kernel(const void* __restr
 
 template <int T, bool OBF>
 static hipError_t launch_dwconv_t(const void* g, StateRef s, int layer, const float* w, const float* b, void* out,
-                                  int B, hipStream_t st) {
+                                  int B, int opk, hipStream_t st) {
   if (s.ring) {
-    hipLaunchKernelGGL((dwconv_ring_kernel<T, OBF>), dim3(B), dim3(kD / 2), 0, st, g, s, layer, w, b, out);
+    hipLaunchKernelGGL((dwconv_ring_kernel<T, OBF>), dim3(B), dim3(kD / 2), 0, st, g, s, layer, w, b, out, opk);
     return hipGetLastError();
   }
   // block shape by batch: 192 channels x 1 stream from B = 1024, else 128 x 1 (profiles/r01_dwconv_sweep.txt,
   // r03_dwconv_sweep.txt)
   if (B >= 1024)
-    hipLaunchKernelGGL((dwconv_kernel<T, OBF, 192, 1>), dim3(B, 2), dim3(192), 0, st, g, s, layer, w, b, out, B);
+    hipLaunchKernelGGL((dwconv_kernel<T, OBF, 192, 1>), dim3(B, 2), dim3(192), 0, st, g, s, layer, w, b, out, B, opk);
   else
-    hipLaunchKernelGGL((dwconv_kernel<T, OBF, 128, 1>), dim3(B, kD / 128), dim3(128), 0, st, g, s, layer, w, b, out, B);
+    hipLaunchKernelGGL((dwconv_kernel<T, OBF, 128, 1>), dim3(B, kD / 128), dim3(128), 0, st, g, s, layer, w, b, out, B,
+                       opk);
   return hipGetLastError();
 }
 
 hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
-                         int T, int B, hipStream_t st) {
-  if (T == kT) return obf ? launch_dwconv_t<kT, true>(g, s, layer, w, b, out, B, st)
-                          : launch_dwconv_t<kT, false>(g, s, layer, w, b, out, B, st);
-  if (T == kT / 2) return obf ? launch_dwconv_t<kT / 2, true>(g, s, layer, w, b, out, B, st)
-                              : launch_dwconv_t<kT / 2, false>(g, s, layer, w, b, out, B, st);
-  if (T == 13) return obf ? launch_dwconv_t<13, true>(g, s, layer, w, b, out, B, st)     // 400 ms chunks
-                          : launch_dwconv_t<13, false>(g, s, layer, w, b, out, B, st);
-  if (T == 6) return obf ? launch_dwconv_t<6, true>(g, s, layer, w, b, out, B, st)
-                         : launch_dwconv_t<6, false>(g, s, layer, w, b, out, B, st);
+                         int T, int B, hipStream_t st, bool out_packed) {
+  if (obf && out_packed) return hipErrorInvalidValue;   // the packed layout is fp32 (gemm_d3's A)
+  const int pk = out_packed;
+  if (T == kT) return obf ? launch_dwconv_t<kT, true>(g, s, layer, w, b, out, B, pk, st)
+                          : launch_dwconv_t<kT, false>(g, s, layer, w, b, out, B, pk, st);
+  if (T == kT / 2) return obf ? launch_dwconv_t<kT / 2, true>(g, s, layer, w, b, out, B, pk, st)
+                              : launch_dwconv_t<kT / 2, false>(g, s, layer, w, b, out, B, pk, st);
+  if (T == 13) return obf ? launch_dwconv_t<13, true>(g, s, layer, w, b, out, B, pk, st)     // 400 ms chunks
+                          : launch_dwconv_t<13, false>(g, s, layer, w, b, out, B, pk, st);
+  if (T == 6) return obf ? launch_dwconv_t<6, true>(g, s, layer, w, b, out, B, pk, st)
+                         : launch_dwconv_t<6, false>(g, s, layer, w, b, out, B, pk, st);
   return hipErrorInvalidValue;
 }
 

@@ -1016,6 +1016,12 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
     if (e == hipSuccess && a.C8 && !c8) return launch_quant_mx(a.C2, a.ldc, a.M, a.N, a.C8, a.C8s, a.ss8, st);
     return e;
   }
+  // fp32 split mode, fragment-packed operands (common.h xpk_off): the consumer is gemm_d3, the producer the fp32 SwiGLU
+  // epilogue of gemm_x3 -- nothing else reads or writes that layout
+  if (a.a_packed) return bf16 ? hipErrorInvalidValue : gemm_d3(a, epi, -1, st);
+  if (a.c_packed && (bf16 || epi != EPI_SWIGLU || !a.W3 || a.a_bf16 || a.c_bf16 || a.c_plane || a.M <= 64 ||
+                     a.ldc % 32 != 0))
+    return hipErrorInvalidValue;
   if (!bf16 && a.W3 && !a.a_bf16 && !a.c_bf16 && !a.rpg && a.K % 64 == 0 && a.lda % 4 == 0 && a.ldc % 4 == 0) {
     // fp32 by exact bf16 splitting (gemm_t.hip gemm_x3); tile per shape from tools/gemm_bench
     // (scripts/x3_sweep.sh, profiles/r01_x3_sweep_b256.jsonl)

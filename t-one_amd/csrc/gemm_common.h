@@ -142,7 +142,9 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const f32x4 w = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
-            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + mrow * p.ldc + (n0 + nl) / 2 + 8 * g + 4 * lh) = w;
+            // c_packed: FFN down's A for gemm_d3 (common.h xpk_off; 4 consecutive columns stay one 16-byte run)
+            const int col = (n0 + nl) / 2 + 8 * g + 4 * lh;
+            if (ok) *reinterpret_cast<f32x4*>(static_cast<float*>(p.C) + act_off(mrow, col, (int)p.ldc, p.c_packed)) = w;
           }
         }
       }

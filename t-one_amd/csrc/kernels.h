@@ -18,6 +18,8 @@ struct Knobs {
                        // bit-identical: the fused form adds the row's squares in another order and multiplies by one
                        // reciprocal per row instead of dividing each element (last-bit differences of the residual)
   int h_blocked;       // TONE_H_BLOCKED=0: the bf16 FFN hidden row-major instead of in 32 x 32 tiles (bit-identical)
+  int d3;              // TONE_D3=0: fp32 N = 384 projections at small M on gemm_x3 instead of gemm_d3 (last-bit changes:
+                       // the K-split partials are added in another order)
 };
 const Knobs& knobs();
 
@@ -86,9 +88,19 @@ struct GemmArgs {
                        // row after the residual add; C and its shadows hold the normalized row
   int h_blocked;       // bf16 FFN hidden h in 32 x 32 tiles (common.h hblk_off): the SWIGLU output C of gemm_xw, the
                        // RESID input A of gemm_rp (the only two kernels that take it; gemm() routes it there or refuses)
+  // fp32 split mode, gemm_d3 (common.h xpk_off / wpk_off): W's planes fragment-packed, A fragment-packed (the consumer),
+  // C written fragment-packed (the fp32 SWIGLU epilogue of gemm_x3, producing FFN down's A)
+  const uint16_t* W3P;
+  int a_packed, c_packed;
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
+// fp32 split mode, STORE / RESID with N = 384 (gemm_d3.hip): fragment-packed operands loaded straight into registers, no
+// LDS staging; variant = wave arrangement / K split / prefetch depth (-1: by shape; hipErrorInvalidValue when the shape
+// does not fit it).  gemm_d3_routed: whether gemm() sends an fp32 projection of this shape there -- the session then has
+// its A written packed by the producer (a_packed) and W packed at load (W3P).
+hipError_t gemm_d3(const GemmArgs& a, int epi, int variant, hipStream_t st);
+bool gemm_d3_routed(int M, int K, int N);
 // Row-panel residual GEMM (gemm_rp.hip): bf16 A / W, N = 384, the fp16 residual stream updated in place with the whole
 // output row per workgroup (optional fused RMSNorm, norm_w); bm = panel rows (0: about one panel per CU)
 hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm = 0);
@@ -237,13 +249,15 @@ struct AttnArgs {
   int reduced;                      // mask offset floor-divided by 2 (layer 14)
   int B;
   int ctx_bf16;
+  int ctx_packed;                   // fp32 only: ctx fragment-packed (common.h xpk_off) for gemm_d3
 };
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 
 // a9: depthwise causal conv k31 with carried state + folded BatchNorm + SiLU; g and out bf16 when obf, else fp32.
 // With s.ring (the resident form) the caches are read from / the new frames written to the stream's ring.
+// out_packed (fp32 only): out fragment-packed (common.h xpk_off) for gemm_d3.
 hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, const float* b, void* out, bool obf,
-                         int T, int B, hipStream_t st);
+                         int T, int B, hipStream_t st, bool out_packed = false);
 
 // flat state <-> resident form (common.h StateRef, tone_session_ring_import / _export): stream i's flat row i <-> slab
 // row rows[i] + ring ring_ids[i]; T / Tr = frames per step outside / inside the reduced block (the layers' phases)

@@ -34,6 +34,7 @@ const Knobs& knobs() {
     r.fp8_normq = env("TONE_FP8_NORMQ", 1) != 0;
     r.rp_norm = env("TONE_RP_NORM", 1) != 0;
     r.h_blocked = env("TONE_H_BLOCKED", 1) != 0;
+    r.d3 = env("TONE_D3", 1) != 0;
     return r;
   }();
   return k;
@@ -120,6 +121,7 @@ struct tone_session {
   float *whead, *bhead;
   LayerW L[16];
   std::map<const void*, const uint16_t*> w3;   // fp32 (split) mode: GEMM weight -> its bf16 planes
+  std::map<const void*, const uint16_t*> w3p;  // fp32 mode, the gemm_d3-routed weights: planes fragment-packed
 
   // activations
   float *wave, *power, *feats, *rA, *rB, *qkv, *kvp, *g, *probs;
@@ -244,7 +246,8 @@ int upload_mx(tone_session* s, MxW* out, const std::vector<float>& v, int N, int
 // GEMM weight in the session's precision (fp32, or bf16 bits).  fp32 (split) mode also uploads the
 // exact three-term bf16 split [3][N][K] (w = w0 + w1 + w2, each term the bf16 rounding of what the
 // previous ones leave) that gemm_x3 reads.
-int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
+// packK > 0 (fp32 mode, the N = 384 projections gemm_d3 can take): also the planes fragment-packed (common.h wpk_off)
+int upload_w(tone_session* s, void** out, const std::vector<float>& v, int packK = 0) {
   if (!bfmode(s)) {
     float* p;
     int rc = upload(s, &p, v);
@@ -265,6 +268,18 @@ int upload_w(tone_session* s, void** out, const std::vector<float>& v) {
     if (rc) return rc;
     HIP_TRY(hipMemcpy(d, pl.data(), pl.size() * 2, hipMemcpyHostToDevice));
     s->w3[p] = d;
+    if (packK > 0 && packK % 32 == 0 && n % ((size_t)32 * packK) == 0) {
+      const int64_t N = (int64_t)(n / packK);
+      std::vector<uint16_t> pk(pl.size());
+      for (int64_t r = 0; r < N; ++r)
+        for (int k = 0; k < packK; ++k)
+          for (int q = 0; q < 3; ++q) pk[wpk_off(r, k, q, packK)] = pl[q * n + (size_t)r * packK + k];
+      uint16_t* dp;
+      rc = dalloc(s, &dp, pk.size());
+      if (rc) return rc;
+      HIP_TRY(hipMemcpy(dp, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+      s->w3p[p] = dp;
+    }
     return TONE_OK;
   }
   std::vector<uint16_t> hb(v.size());
@@ -394,7 +409,7 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
               float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr,
               bool mx_out = false, const DwFuse* dw = nullptr, const AttFuse* att = nullptr,
-              const float* norm_w = nullptr, bool h_blocked = false) {
+              const float* norm_w = nullptr, bool h_blocked = false, bool a_packed = false, bool c_packed = false) {
   GemmArgs a{};   // value-initialised: every field not set below is zero
   a.norm_w = norm_w;
   a.h_blocked = h_blocked;
@@ -432,7 +447,11 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   if (s->precision == TONE_PRECISION_FP32) {
     auto it = s->w3.find(W);
     a.W3 = it == s->w3.end() ? nullptr : it->second;
+    auto ip = s->w3p.find(W);
+    a.W3P = ip == s->w3p.end() ? nullptr : ip->second;
   }
+  a.a_packed = a_packed;
+  a.c_packed = c_packed;
   LAUNCH(fam, gemm(a, epi, bf, st));
   return TONE_OK;
 }
@@ -547,6 +566,11 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     // tiles (common.h hblk_off), whole-KiB stores out of gemm_xw instead of 32-byte row segments
     const bool h_blocked = bf && !f8 && knobs().h_blocked && gemm_rp_routed(M, kDff) && (M + 255) / 256 >= 40;
     const bool q8_after_norm = f8n && l != 6 && l < 14;
+    // fp32 mode, the N = 384 projections routed to gemm_d3 (M = B T in its range): their A operands (h, ctx, the
+    // depthwise conv output) written fragment-packed by their producers (common.h xpk_off)
+    const bool f32m = s->precision == TONE_PRECISION_FP32;
+    const bool pk_h = f32m && gemm_d3_routed(M, kDff, D) && s->w3p.count(w.w2[0]) && s->w3p.count(w.w2[1]);
+    const bool pk_d = f32m && gemm_d3_routed(M, D, D) && s->w3p.count(w.wo) && s->w3p.count(w.wpw2);
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
     // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
     // up-projection's epilogue
@@ -564,10 +588,10 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
                        0.5f, false, xs, nullptr, nullptr, fuse ? q8_after_norm : q8_fresh, fuse ? w.norm_out : nullptr);
       }
       CALL(gemm_call(s, st, "gemm_ffn_up", xa, D, w.w13[f], s->h, kDff, w.b13[f], M, 2 * kDff, D, EPI_SWIGLU, 1, nullptr,
-                     1.0f, true, true, nullptr, false, nullptr, nullptr, nullptr, h_blocked));
+                     1.0f, true, true, nullptr, false, nullptr, nullptr, nullptr, h_blocked, false, pk_h));
       // FFN2's down-projection on the row-panel kernel also applies the block-final RMSNorm (norm_out)
       return gemm_call(s, st, "gemm_ffn_down", s->h, kDff, w.w2[f], x, D, w.b2[f], M, D, kDff, EPI_RESID, 0, x, 0.5f, true,
-                       false, xs, false, nullptr, nullptr, f == 1 && norm_fused ? w.norm_out : nullptr, h_blocked);
+                       false, xs, false, nullptr, nullptr, f == 1 && norm_fused ? w.norm_out : nullptr, h_blocked, pk_h);
     };
     CALL(ffn(0));
     // MHSA (conformer_blocks.py:816-825)
@@ -637,9 +661,10 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       CALL(gemm_call(s, st, "gemm_attn_out_ctx", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, false,
                      false, nullptr, false, nullptr, &af));
     } else {
+      aa.ctx_packed = pk_d;
       LAUNCH("attention", launch_attention(aa, st));
       CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false,
-                     xs));
+                     xs, false, nullptr, nullptr, nullptr, false, pk_d));
     }
     q8_fresh = false;
     // Convolution module (conformer_blocks.py:827-830)
@@ -652,10 +677,11 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     } else {
       CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true,
                      true));   // g in bf16 in the bf16 / fp8 modes (fp32 in fp32 mode: gemm_call drops c_bf16 there)
-      LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st));
+      LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st, pk_d));
     }
     // fp8 mode: pw2 also emits FFN2's MXFP8 operand
-    CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs, f8n));
+    CALL(gemm_call(s, st, "gemm_pw2", s->d, D, w.wpw2, x, D, w.bpw2, M, D, D, EPI_RESID, 0, x, 1.0f, true, false, xs, f8n,
+                   nullptr, nullptr, nullptr, false, pk_d));
     q8_fresh = f8n;
     if (s->debug_stop == 100 + l) {   // FFN2's MXFP8 operand: the pw2 epilogue's, or quant_mx's with the fusion off
       if (f8 && !f8n) LAUNCH("quant_mx", launch_quant_mx(xs, D, M, D, s->a8, s->a8s, s->ss8, st));
@@ -831,7 +857,7 @@ int finalize_weights(tone_session* s) {
         }
       CALL(upload_w(s, &lw.w13[f], w13));
       CALL(upload(s, &lw.b13[f], b13));
-      CALL(upload_w(s, &lw.w2[f], *w2));
+      CALL(upload_w(s, &lw.w2[f], *w2, kDff));
       if (s->precision == TONE_PRECISION_FP8) {
         CALL(upload_mx(s, &lw.mx13[f], w13, 2 * kDff, D));
         CALL(upload_mx(s, &lw.mx2[f], *w2, D, kDff));
@@ -891,7 +917,7 @@ int finalize_weights(tone_session* s) {
       CALL(upload(s, &lw.bkv, bkv));
       CALL(upload(s, &lw.norm_att, *natt));
     }
-    CALL(upload_w(s, &lw.wo, *wo));
+    CALL(upload_w(s, &lw.wo, *wo, kD));
     CALL(upload(s, &lw.bo, *bo));
 
     const std::string c = p + "conv.";
@@ -927,7 +953,7 @@ int finalize_weights(tone_session* s) {
     }
     CALL(upload(s, &lw.wdw, wd));
     CALL(upload(s, &lw.bdw, bd));
-    CALL(upload_w(s, &lw.wpw2, *pw2));
+    CALL(upload_w(s, &lw.wpw2, *pw2, kD));
     CALL(upload(s, &lw.bpw2, *pb2));
     CALL(upload(s, &lw.norm_out, *nout));
   }
@@ -948,9 +974,9 @@ int finalize_weights(tone_session* s) {
   CALL(dalloc(s, reinterpret_cast<float**>(&s->xn), MB * kTMax * D));
   CALL(dalloc(s, reinterpret_cast<float**>(&s->kv), MB * (30 + kTMax) * D));
   CALL(dalloc(s, &s->kvp, MB * (30 + kTMax) * 2 * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->ctx), MB * kTMax * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->ctx), (MB * kTMax + 32) * D));   // + 32 rows: the packed form's last block
   CALL(dalloc(s, &s->g, MB * kTMax * D));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->d), MB * kTMax * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->d), (MB * kTMax + 32) * D));
   CALL(dalloc(s, &s->probs, MB * kHeads * kTMax * (30 + kTMax)));
   CALL(dalloc(s, reinterpret_cast<float**>(&s->yred), MB * kTrMax * 4 * D));
   CALL(dalloc(s, &s->xbA, MB * kTMax * D));

@@ -162,6 +162,13 @@ __global__ void q8_cmp_kernel(const uint8_t* q, const uint8_t* s, const float* s
 }
 
 // the blocked FFN hidden (common.h hblk_off; HBLK=1): row-major -> blocked and back, bf16 [rows][ld]
+// fragment-packed fp32 rows (common.h xpk_off, gemm_d3's A / the fp32 SwiGLU epilogue's c_packed) back to row-major
+__global__ void xunpack_kernel(const float* src, float* dst, int64_t rows, int ld) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * ld) return;
+  dst[i] = src[xpk_off(i / ld, (int)(i % ld), ld)];
+}
+
 __global__ void hblk_kernel(const uint16_t* src, uint16_t* dst, int64_t rows, int ld, int to_blocked) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * ld) return;
@@ -315,6 +322,8 @@ int main(int argc, char** argv) {
   float *Af, *Wf;
   uint16_t* W3;   // the three bf16 planes of Wf (gemm_x3)
   uint16_t* A3;   // the three bf16 planes of Af (gemm_x3 with a pre-split A, variants 60-65)
+  uint16_t* W3P;  // W3 fragment-packed (gemm_d3)
+  float* Afp;     // Af fragment-packed (gemm_d3 under PACKX=1)
   {
     std::vector<float> fa(hA.size()), fw(hW.size());
     for (size_t i = 0; i < hA.size(); ++i) { uint32_t u = (uint32_t)hA[i] << 16; memcpy(&fa[i], &u, 4); }
@@ -343,6 +352,20 @@ int main(int argc, char** argv) {
       a3[i] = h; a3[fa.size() + i] = m; a3[2 * fa.size() + i] = to_bf16(r1 - bf2f(m));
     }
     CK(hipMalloc(&A3, a3.size() * 2));
+    // gemm_d3's fragment-packed operands: W's planes always, A's rows under PACKX=1 (padding rows NaN: they must
+    // not reach any stored output)
+    const size_t mp = (size_t)(M + 31) / 32 * 32;
+    std::vector<uint16_t> w3p(w3.size());
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < K; ++k)
+        for (int pl = 0; pl < 3; ++pl) w3p[wpk_off(n, k, pl, K)] = w3[(size_t)pl * fw.size() + (size_t)n * K + k];
+    CK(hipMalloc(&W3P, w3p.size() * 2));
+    CK(hipMemcpy(W3P, w3p.data(), w3p.size() * 2, hipMemcpyHostToDevice));
+    std::vector<float> afp(mp * K, std::nanf(""));
+    for (int m = 0; m < M; ++m)
+      for (int k = 0; k < K; ++k) afp[xpk_off(m, k, K)] = fa[(size_t)m * K + k];
+    CK(hipMalloc(&Afp, afp.size() * 4));
+    CK(hipMemcpy(Afp, afp.data(), afp.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(A3, a3.data(), a3.size() * 2, hipMemcpyHostToDevice));
   }
   CK(hipMemcpy(A, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
@@ -384,6 +407,7 @@ int main(int argc, char** argv) {
   float* refn = nullptr;
   if (normw) CK(hipMalloc(&refn, (size_t)M * nout * 4));
   uint16_t *Ablk = nullptr, *Cun = nullptr;
+  float* Cunf = nullptr;
   Q8Bufs q8b;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -405,11 +429,17 @@ int main(int argc, char** argv) {
     if (vv <= -300 && getenv("XSDBG")) a.dbg = atoi(getenv("XSDBG"));   // gemm_xw ablations
     // RESID writes C in place of R in the session; here R is separate so repeated launches are idempotent
     CK(hipMemset(C, 0, (size_t)M * nout * 4));
-    const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (v >= 30 && v < 50) || (v >= 50 && v < 90);
+    const bool f32 = (vv == -2) || (vv == -3) || (vv == -4) || (vv <= -499) || (v >= 30 && v < 50) || (v >= 50 && v < 90);
     // -2: gemm() fp32 routing with W planes, -3: without, -4: with W and A planes
-    a.W3 = (vv == -2 || vv == -4 || (v >= 50 && v < 90)) ? W3 : nullptr;
+    a.W3 = (vv == -2 || vv == -4 || vv <= -499 || (v >= 50 && v < 90)) ? W3 : nullptr;
     a.a_plane = (vv == -4 || (v >= 60 && v < 70)) ? (int64_t)M * K : 0;
     a.A = a.a_plane ? (const void*)A3 : f32 ? (const void*)Af : (const void*)A;
+    a.W3P = W3P;
+    // PACKX=1: gemm_d3 reads A fragment-packed; CPACK=1: an fp32 SWIGLU variant writes C fragment-packed (unpacked
+    // for the check)
+    a.a_packed = vv <= -499 && getenv("PACKX") && atoi(getenv("PACKX"));   // -499: gemm()'s routing (gemm_d3 by shape)
+    if (a.a_packed) a.A = Afp;
+    a.c_packed = f32 && epi == 2 && vv > -300 && getenv("CPACK") && atoi(getenv("CPACK"));
     a.W = f32 ? (const void*)Wf : (const void*)W;
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
@@ -443,7 +473,9 @@ int main(int argc, char** argv) {
       a.C8 = nullptr; a.C8s = nullptr; a.ss8 = nullptr;
     }
     auto launch = [&]() {
-      return vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
+      return vv <= -500 ? gemm_d3(a, epi, -500 - vv, 0)   // -500 - c: gemm_d3 variant c
+             : vv == -499 ? gemm(a, epi, false, 0)
+             : vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
              : (v >= 90 && v <= 98) ? gemm_rp(a, 0, kRpRows[v - 90])   // 90: auto panel rows, 91-98: 16 .. 160
              : v >= 70 ? gemm_x3(a, epi, v - 70, 0)   // 70-89: fp32 A, any x3 tile variant
@@ -460,6 +492,12 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     CK(hipMemset(err, 0, 4));
     const void* Cchk = C;
+    if (a.c_packed) {
+      if (!Cunf) CK(hipMalloc(&Cunf, (size_t)M * nout * 4));
+      hipLaunchKernelGGL(xunpack_kernel, dim3((unsigned)(((int64_t)M * nout + 255) / 256)), dim3(256), 0, 0,
+                         static_cast<const float*>(C), Cunf, (int64_t)M, nout);
+      Cchk = Cunf;
+    }
     if (hblk && vv <= -300) {   // the blocked output, back to row-major for the check
       if (!Cun) CK(hipMalloc(&Cun, (size_t)M * nout * 2));
       hipLaunchKernelGGL(hblk_kernel, dim3((unsigned)(((int64_t)M * nout + 255) / 256)), dim3(256), 0, 0,

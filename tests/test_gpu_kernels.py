@@ -139,6 +139,27 @@ def test_fp32_routes_match_reference(M, K, N, epi, rs):
     assert r["max_rel_err"] < 2e-5, r
 
 
+# fp32 mode's N = 384 projections where the session routes them to gemm_d3 (gemm_d3_routed: attn-out / pw2 K = 384, FFN
+# down K = 1536, M = B T from 65 to 4096): A and W fragment-packed (common.h xpk_off / wpk_off; the padding rows of A's
+# last 32-row block NaN, so a read of them that reached an output would show), through gemm()'s own routing, full fp32
+# operands against fp64
+@pytest.mark.parametrize("M", [2560, 1280, 3328, 1536, 640, 320, 100])
+@pytest.mark.parametrize("K", [384, 1536])
+def test_fp32_d3_packed_matches_reference(M, K):
+    _gpu()
+    r = _run(M, K, 384, 1, -499, {"FULLF32": 1, "NOC2": 1, "PACKX": 1})
+    assert r["max_rel_err"] < 2e-5, r
+
+
+# ... and the producer side of FFN down's packed A: the fp32 SwiGLU epilogue (gemm_x3) writing h fragment-packed, read
+# back through the inverse map
+@pytest.mark.parametrize("M", [2560, 1280, 3328, 1536, 640, 100])
+def test_fp32_swiglu_packed_output_matches_reference(M):
+    _gpu()
+    r = _run(M, 384, 3072, 2, -2, {"FULLF32": 1, "NOC2": 1, "ROWSCALE": 1, "CPACK": 1})
+    assert r["max_rel_err"] < 2e-5, r
+
+
 # the bf16 step's GEMMs through gemm()'s routing below the large-batch kernels (gemm_glds, gemm_t; B = 512 .. 1638)
 @pytest.mark.parametrize("M", [10240, 5120, 2560])
 @pytest.mark.parametrize("K,N,epi,rs", FP32_OPS)
