@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(CPW) dwconv_kernel(const void* __restrict__ g,
 // T new frames are written back, over the T oldest (ring rows ph .. ph + T - 1), instead of the whole shifted window:
 // 30 + 3 T frames of HBM traffic per stream and layer instead of 60 + 2 T.  Arithmetic identical to dwconv_kernel
 // (same fma order, same SiLU forms): outputs and the exported state are bit-identical to the flat form's.
-template <int T, bool OBF>
+template <int T, bool OBF, bool NTH>
 __global__ void __launch_bounds__(kD / 2) dwconv_ring_kernel(const void* __restrict__ g, StateRef s, int layer,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
                                                             void* __restrict__ out, int opk) {
@@ -547,7 +547,8 @@ __global__ void __launch_bounds__(kD / 2) dwconv_ring_kernel(const void* __restr
 #pragma unroll
   for (int i = 0; i < kConvS; ++i) {
     const int r = ph + i < kConvS ? ph + i : ph + i - kConvS;
-    const __half2 h = *reinterpret_cast<const __half2*>(rg + (int64_t)r * kD);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(rg + (int64_t)r * kD);
+    const __half2 h = __builtin_bit_cast(__half2, NTH ? __builtin_nontemporal_load(src) : *src);
     x[i][0] = __low2float(h);
     x[i][1] = __high2float(h);
   }
@@ -584,7 +585,10 @@ __global__ void __launch_bounds__(kD / 2) dwconv_ring_kernel(const void* __restr
 #pragma unroll
   for (int j = 0; j < T; ++j) {
     const int r = ph + j < kConvS ? ph + j : ph + j - kConvS;
-    *reinterpret_cast<__half2*>(rg + (int64_t)r * kD) = __floats2half2_rn(x[kConvS + j][0], x[kConvS + j][1]);
+    const __half2 v = __floats2half2_rn(x[kConvS + j][0], x[kConvS + j][1]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(rg + (int64_t)r * kD);
+    if constexpr (NTH) __builtin_nontemporal_store(__builtin_bit_cast(uint32_t, v), dst);
+    else *dst = __builtin_bit_cast(uint32_t, v);
   }
 }
 
@@ -592,7 +596,13 @@ template <int T, bool OBF>
 static hipError_t launch_dwconv_t(const void* g, StateRef s, int layer, const float* w, const float* b, void* out,
                                   int B, int opk, hipStream_t st) {
   if (s.ring) {
-    hipLaunchKernelGGL((dwconv_ring_kernel<T, OBF>), dim3(B), dim3(kD / 2), 0, st, g, s, layer, w, b, out, opk);
+    // the ring's rows read / written non-temporally (each read once per step, 16 layers apart: nothing worth keeping in
+    // L2 / MALL): bf16 B = 4096 dwconv 615 -> 586 us per step, the step 8615 -> 8500 (the other kernels' lines stay
+    // cached; profiles/r06_ring_nt_ab.txt); TONE_RING_NT=0 turns it off
+    if (knobs().ring_nt)
+      hipLaunchKernelGGL((dwconv_ring_kernel<T, OBF, true>), dim3(B), dim3(kD / 2), 0, st, g, s, layer, w, b, out, opk);
+    else
+      hipLaunchKernelGGL((dwconv_ring_kernel<T, OBF, false>), dim3(B), dim3(kD / 2), 0, st, g, s, layer, w, b, out, opk);
     return hipGetLastError();
   }
   // block shape by batch: 192 channels x 1 stream from B = 1024, else 128 x 1 (profiles/r01_dwconv_sweep.txt,

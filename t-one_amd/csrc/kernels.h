@@ -18,6 +18,7 @@ struct Knobs {
                        // bit-identical: the fused form adds the row's squares in another order and multiplies by one
                        // reciprocal per row instead of dividing each element (last-bit differences of the residual)
   int h_blocked;       // TONE_H_BLOCKED=0: the bf16 FFN hidden row-major instead of in 32 x 32 tiles (bit-identical)
+  int ring_nt;         // TONE_RING_NT=0: dwconv_ring reads / writes the ring rows through the caches (bit-identical)
   int d3;              // TONE_D3=0: fp32 N = 384 projections at small M on gemm_x3 instead of gemm_d3 (last-bit changes:
                        // the K-split partials are added in another order)
 };

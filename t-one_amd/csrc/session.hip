@@ -35,6 +35,7 @@ const Knobs& knobs() {
     r.rp_norm = env("TONE_RP_NORM", 1) != 0;
     r.h_blocked = env("TONE_H_BLOCKED", 1) != 0;
     r.d3 = env("TONE_D3", 1) != 0;
+    r.ring_nt = env("TONE_RING_NT", 1) != 0;
     return r;
   }();
   return k;
