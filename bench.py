@@ -126,7 +126,7 @@ def measured_traffic(family: str, precision: str, batch: int):
     """HBM bytes per launch of a GEMM family ("gemm_ffn_up", or "resid" = every EPI_RESID launch) from the
     committed rocprofv3 PMC summary (scripts/pmc_traffic.sh + scripts/traffic_summary.py: FETCH_SIZE x2 +
     WRITE_SIZE, gfx950 correction), or (None, None) when no summary covers this precision / batch / family."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):   # the newest round's summary first
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):   # the newest round's summary first
         path = os.path.join(ROOT, "profiles", f"{rnd}_traffic_{precision}_b{batch}.json")
         try:
             with open(path) as fh:

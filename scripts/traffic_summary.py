@@ -16,7 +16,8 @@ UP = {  # SWIGLU instantiations: EPI_SWIGLU = 2
 # EPI_RESID = 1, in any GEMM kernel family; every gemm_rp_kernel launch
 RESID = (r"(gemm_x3_kernel<tone::(?:\(anonymous namespace\)::)?XT<[^>]*>, 1,|gemm_glds_kernel<tone::(?:\(anonymous namespace\)::)?Tile<[^>]*>, 1,|gemm_kernel<tone::(?:\(anonymous namespace\)::)?Tile<[^>]*>, 1,"
          r"|gemm_t_kernel<tone::(?:\(anonymous namespace\)::)?TT<[^>]*>, 1,|gemm_f32t_kernel<[^>]*>, 1,|gemm_mx_kernel<\d+, 1,"
-         r"|gemm_rp_kernel<)")   # the row-panel kernel (round 5) is RESID only
+         r"|gemm_rp_kernel<"     # the row-panel kernel (round 5) is RESID only
+         r"|gemm_d3_kernel<\d+, \d+, \d+, \d+, 1,)")   # fp32 direct-load kernel (round 6): <WM, WN, WK, D, EPI, XP>
 
 
 def per_launch(sub, pat):

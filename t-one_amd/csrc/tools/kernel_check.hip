@@ -543,6 +543,21 @@ __global__ void ref_dwconv_kernel(const void* g, int gty, StateRef s, int layer,
   for (int k = 0; k < kConvS; ++k) ex[(int64_t)b * kD * kConvS + c * kConvS + k] = __float2half_rn(x[T + k]);
 }
 
+// "_pk" checks (fp32): the output written fragment-packed for gemm_d3 (common.h xpk_off), unpacked here for the compare
+static bool g_pk = false;
+__global__ void xunpack_kernel(const float* src, float* dst, int64_t rows, int ld) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * ld) return;
+  dst[i] = src[xpk_off(i / ld, (int)(i % ld), ld)];
+}
+static const void* unpacked(const void* out, int64_t rows) {
+  if (!g_pk) return out;
+  float* u = pool.get<float>(rows * kD);
+  hipLaunchKernelGGL(xunpack_kernel, grid1(rows * kD), dim3(256), 0, 0, static_cast<const float*>(out), u, rows, kD);
+  CK(hipDeviceSynchronize());
+  return u;
+}
+
 static void check_dwconv(int B, int T, bool bf, Report& rep) {
   Slab sl;
   sl.make(B);
@@ -552,7 +567,7 @@ static void check_dwconv(int B, int T, bool bf, Report& rep) {
   const void* g = bf ? (const void*)to_bf16(gf, M * kD) : (const void*)gf;
   const float* w = rand_f32(kConvK * kD, 32, 0.2f);
   const float* bias = rand_f32(kD, 33, 0.2f);
-  void* out = bf ? (void*)pool.get<uint16_t>(M * kD) : (void*)pool.get<float>(M * kD);
+  void* out = bf ? (void*)pool.get<uint16_t>(M * kD) : (void*)pool.get<float>((M + 32) * kD);
   float* ref = pool.get<float>(M * kD);
   Secs secs{};
   secs.s[0] = {kOffConv + (int64_t)layer * kD * kConvS, (int64_t)kD * kConvS};
@@ -562,8 +577,9 @@ static void check_dwconv(int B, int T, bool bf, Report& rep) {
   hipLaunchKernelGGL(ref_dwconv_kernel, grid1((int64_t)B * kD), dim3(256), 0, 0, g, bf ? 1 : 0, sl.ref(), layer, w, bias, T,
                      ref, exps, B);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([=] { return launch_dwconv(g, sl.ref(), layer, w, bias, out, bf, T, B, 0); });
-  rep.out("out", out, bf ? 1 : 0, kD, ref, M, kD);
+  const bool pk = g_pk;
+  rep.us = time_once([=] { return launch_dwconv(g, sl.ref(), layer, w, bias, out, bf, T, B, 0, pk); });
+  rep.out("out", unpacked(out, M), bf ? 1 : 0, kD, ref, M, kD);
   rep.state(sl, secs, exps);
 }
 
@@ -615,13 +631,14 @@ static void check_dwconv_ring(int B, int T, bool bf, Report& rep) {
   const void* g = bf ? (const void*)to_bf16(gf, M * kD) : (const void*)gf;
   const float* w = rand_f32(kConvK * kD, 32, 0.2f);
   const float* bias = rand_f32(kD, 33, 0.2f);
-  void* out = bf ? (void*)pool.get<uint16_t>(M * kD) : (void*)pool.get<float>(M * kD);
+  void* out = bf ? (void*)pool.get<uint16_t>(M * kD) : (void*)pool.get<float>((M + 32) * kD);
   float* ref = pool.get<float>(M * kD);
   hipLaunchKernelGGL(ref_dwconv_ring_kernel, grid1((int64_t)B * kD), dim3(256), 0, 0, g, bf ? 1 : 0, sr, ring0, layer, w, bias,
                      T, ref, ring_exp, B);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([=] { return launch_dwconv(g, sr, layer, w, bias, out, bf, T, B, 0); });
-  rep.out("out", out, bf ? 1 : 0, kD, ref, M, kD);
+  const bool pk = g_pk;
+  rep.us = time_once([=] { return launch_dwconv(g, sr, layer, w, bias, out, bf, T, B, 0, pk); });
+  rep.out("out", unpacked(out, M), bf ? 1 : 0, kD, ref, M, kD);
   // every ring element (all layers, the unused ring too) against the expected rings: bytes
   int* bad = pool.get<int>(1);
   CK(hipMemset(bad, 0, 4));
@@ -774,15 +791,16 @@ static void check_attention(int B, int T, int S, bool recompute, bool bf, Report
   } else {
     a.probs = S == 0 ? pool.get<float>(np) : nullptr;   // written by layers 0 / 7 only (session.hip)
   }
-  void* ctx = bf ? (void*)pool.get<uint16_t>((int64_t)B * T * kD) : (void*)pool.get<float>((int64_t)B * T * kD);
+  void* ctx = bf ? (void*)pool.get<uint16_t>((int64_t)B * T * kD) : (void*)pool.get<float>(((int64_t)B * T + 32) * kD);
   a.ctx = ctx;
+  a.ctx_packed = g_pk;
   float* ref = pool.get<float>((int64_t)B * T * kD);
   AttnArgs ar = a;
   hipLaunchKernelGGL(ref_attention_kernel, grid1((int64_t)B * kHeads * T, 64), dim3(64), 0, 0, ar, ty, ref,
                      recompute && a.probs ? probs_ref : nullptr);
   CK(hipDeviceSynchronize());
   rep.us = time_once([=] { return launch_attention(a, 0); });
-  rep.out("ctx", ctx, ty, kD, ref, (int64_t)B * T, kD);
+  rep.out("ctx", unpacked(ctx, (int64_t)B * T), ty, kD, ref, (int64_t)B * T, kD);
   if (recompute && a.probs) rep.out("probs", a.probs, 0, TK, probs_ref, (int64_t)B * kHeads * T, TK);
   // the attention kernels read the state (mhsa_len) and write none of it
   Secs none{};
@@ -1139,7 +1157,8 @@ int main(int argc, char** argv) {
   if (argc < 3) {
     fprintf(stderr,
             "usage: %s <check> <B> [T]\n  checks: sub_conv sub1_f32 sub1_f32_400 sub1_bf16_400 conv2_f32 conv2_f32_400 "
-            "conv2_bf16_400 dwconv[_bf16] attn_rec[_bf16] (T S) attn_shared[_bf16] kv[_bf16] (T S) reduce[_bf16] "
+            "conv2_bf16_400 dwconv[_bf16|_pk] dwconv_ring[_bf16|_pk] attn_rec[_bf16|_pk] (T S) attn_shared[_bf16|_pk] "
+            "kv[_bf16] (T S) kv_ring[_bf16] (T S) reduce[_bf16] "
             "upsample[_r16] head[_r16] (rows) rmsnorm[_r16|_q8] (rows)\n",
             argv[0]);
     return 2;
@@ -1154,6 +1173,11 @@ int main(int argc, char** argv) {
   rep.T = T;
   auto has = [&](const char* suf) { return ck.size() >= strlen(suf) && ck.compare(ck.size() - strlen(suf), strlen(suf), suf) == 0; };
   const bool bf = has("_bf16") || has("_bf16_400");
+  g_pk = has("_pk");   // fp32 dwconv / attention: the packed output gemm_d3 reads
+  if (g_pk && bf) {
+    fprintf(stderr, "the packed layout is fp32 only\n");
+    return 2;
+  }
   if (ck == "sub_conv") check_pre("sub_conv", B, 2400, true, rep);
   else if (ck == "sub1_f32") check_pre("sub1", B, 2400, false, rep);
   else if (ck == "sub1_f32_400") check_pre("sub1", B, 3200, false, rep);

@@ -235,8 +235,11 @@ def test_conv2_every_element(check, B, tol):
     assert r["outputs"]["flat"] < tol, r
 
 
+# "_pk": fp32 with the output fragment-packed for gemm_d3 (common.h xpk_off; the step's layout at M = B T > 64), read
+# back through the inverse map
 DW_CASES = [(4096, t, "dwconv_bf16", 1e-2) for t in (10, 5, 13, 6)] + [(2048, 10, "dwconv_bf16", 1e-2)] + \
-           [(256, t, "dwconv", 1e-5) for t in (10, 5, 13, 6)] + [(1, 10, "dwconv", 1e-5)]
+           [(256, t, "dwconv", 1e-5) for t in (10, 5, 13, 6)] + [(1, 10, "dwconv", 1e-5)] + \
+           [(256, t, "dwconv_pk", 1e-5) for t in (10, 5, 13, 6)] + [(9, 10, "dwconv_pk", 1e-5)]   # B coprime with 7 (the check's row permutation)
 
 
 @pytest.mark.parametrize("B,T,check,tol", DW_CASES)
@@ -251,7 +254,8 @@ def test_dwconv_every_element(B, T, check, tol):
 @pytest.mark.parametrize("B,T,check,tol", [(4096, 10, "dwconv_ring_bf16", 1e-2), (4096, 5, "dwconv_ring_bf16", 1e-2),
                                             (2048, 13, "dwconv_ring_bf16", 1e-2), (2048, 6, "dwconv_ring_bf16", 1e-2),
                                             (256, 10, "dwconv_ring", 1e-5), (256, 5, "dwconv_ring", 1e-5),
-                                            (1, 10, "dwconv_ring", 1e-5)])
+                                            (1, 10, "dwconv_ring", 1e-5), (256, 10, "dwconv_ring_pk", 1e-5),
+                                            (256, 5, "dwconv_ring_pk", 1e-5), (256, 13, "dwconv_ring_pk", 1e-5)])
 def test_dwconv_ring_every_element(B, T, check, tol):
     """The resident-form depthwise conv (cache frame i at ring row (n T + i) mod 30, the T new frames written over the T
     oldest): output, and every byte of every ring (the other rows, layers and the unused ring unchanged)."""
@@ -264,7 +268,7 @@ REC_TS = [(10, 0), (5, 0), (5, 15), (10, 30), (13, 0), (6, 0), (6, 15), (13, 30)
 
 
 @pytest.mark.parametrize("T,S", REC_TS)
-@pytest.mark.parametrize("check,B,tol", [("attn_rec_bf16", 4096, 1e-2), ("attn_rec", 256, 5e-5)])
+@pytest.mark.parametrize("check,B,tol", [("attn_rec_bf16", 4096, 1e-2), ("attn_rec", 256, 5e-5), ("attn_rec_pk", 256, 5e-5)])
 def test_attention_rec_every_element(T, S, check, B, tol):
     """Recomputing layers (q/k LayerNorm, RoPE, masked softmax, P V; submodules.py:204-271) for every instantiated
     (T, S); the probabilities the shared layers reuse, where written; no state write."""
@@ -277,7 +281,8 @@ def test_attention_rec_every_element(T, S, check, B, tol):
 
 
 @pytest.mark.parametrize("T", [10, 5, 13, 6])
-@pytest.mark.parametrize("check,B,tol", [("attn_shared_bf16", 4096, 1e-2), ("attn_shared", 256, 1e-5)])
+@pytest.mark.parametrize("check,B,tol", [("attn_shared_bf16", 4096, 1e-2), ("attn_shared", 256, 1e-5),
+                                         ("attn_shared_pk", 256, 1e-5)])
 def test_attention_shared_every_element(T, check, B, tol):
     _gpu()
     r = _check(check, B, T)
