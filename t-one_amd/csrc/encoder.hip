@@ -16,7 +16,7 @@ template <bool R16>
 __global__ void __launch_bounds__(256) rmsnorm_kernel(void* __restrict__ x, const float* __restrict__ w, int rows,
                                                       uint16_t* __restrict__ shadow, int64_t plane,
                                                       uint8_t* __restrict__ q8, uint8_t* __restrict__ s8,
-                                                      float* __restrict__ ss8) {
+                                                      float* __restrict__ ss8, float* __restrict__ xp) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -35,6 +35,7 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(void* __restrict__ x, cons
   for (int i = 0; i < 6; ++i) {
     const float y = w[lane + 64 * i] * (v[i] / den);
     store_res<R16>(x, xr + lane + 64 * i, y);
+    if (!R16 && xp) xp[xpk_off(row, lane + 64 * i, kD)] = y;
     if (shadow) store_shadow(shadow, plane, (int64_t)row * kD + lane + 64 * i, y);
     if (q8) {
       // fp8 mode: the MXFP8 form of the bf16 shadow row for the next layer's FFN up-projection, as
@@ -58,11 +59,14 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(void* __restrict__ x, cons
 }
 
 hipError_t launch_rmsnorm(void* x, const float* w, int rows, uint16_t* shadow, int64_t plane, bool r16, hipStream_t st,
-                          uint8_t* q8, uint8_t* s8, float* ss8) {
+                          uint8_t* q8, uint8_t* s8, float* ss8, float* xp) {
+  if (r16 && xp) return hipErrorInvalidValue;   // the packed copy is fp32 (gemm_d3n's A)
   if (r16)
-    hipLaunchKernelGGL(rmsnorm_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8);
+    hipLaunchKernelGGL(rmsnorm_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8,
+                       xp);
   else
-    hipLaunchKernelGGL(rmsnorm_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8);
+    hipLaunchKernelGGL(rmsnorm_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, rows, shadow, plane, q8, s8, ss8,
+                       xp);
   return hipGetLastError();
 }
 
@@ -638,7 +642,7 @@ hipError_t launch_dwconv(const void* g, StateRef s, int layer, const float* w, c
 template <bool OBF, int T>
 __global__ void __launch_bounds__(256) reduce_conv_kernel(const void* __restrict__ x, StateRef s,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
-                                                          void* __restrict__ y, int B) {
+                                                          void* __restrict__ y, int B, int ypk) {
   constexpr int TR = (T + 1 - 3) / 2 + 1;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= B * kD) return;
@@ -651,17 +655,20 @@ __global__ void __launch_bounds__(256) reduce_conv_kernel(const void* __restrict
     const int o = 4 * c + q;
     const float w0 = w[o * 3], w1 = w[o * 3 + 1], w2 = w[o * 3 + 2], bo = bias[o];
     for (int t = 0; t < TR; ++t)
-      store_act<OBF>(y, ((int64_t)b * TR + t) * (4 * kD) + o, bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2]);
+      store_act<OBF>(y, act_off((int64_t)b * TR + t, o, 4 * kD, !OBF && ypk),
+                     bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2]);
   }
 }
 
 hipError_t launch_reduce_conv(const void* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
-                              int T, hipStream_t st) {
+                              int T, hipStream_t st, bool y_packed) {
+  if (obf && y_packed) return hipErrorInvalidValue;   // the packed layout is fp32 (gemm_d3's A)
   const dim3 grid((B * kD + 255) / 256), block(256);
-  if (T == kT && obf) hipLaunchKernelGGL((reduce_conv_kernel<true, kT>), grid, block, 0, st, x, s, w, b, y, B);
-  else if (T == kT) hipLaunchKernelGGL((reduce_conv_kernel<false, kT>), grid, block, 0, st, x, s, w, b, y, B);
-  else if (T == 13 && obf) hipLaunchKernelGGL((reduce_conv_kernel<true, 13>), grid, block, 0, st, x, s, w, b, y, B);
-  else if (T == 13) hipLaunchKernelGGL((reduce_conv_kernel<false, 13>), grid, block, 0, st, x, s, w, b, y, B);
+  const int pk = y_packed;
+  if (T == kT && obf) hipLaunchKernelGGL((reduce_conv_kernel<true, kT>), grid, block, 0, st, x, s, w, b, y, B, pk);
+  else if (T == kT) hipLaunchKernelGGL((reduce_conv_kernel<false, kT>), grid, block, 0, st, x, s, w, b, y, B, pk);
+  else if (T == 13 && obf) hipLaunchKernelGGL((reduce_conv_kernel<true, 13>), grid, block, 0, st, x, s, w, b, y, B, pk);
+  else if (T == 13) hipLaunchKernelGGL((reduce_conv_kernel<false, 13>), grid, block, 0, st, x, s, w, b, y, B, pk);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -672,7 +679,8 @@ hipError_t launch_reduce_conv(const void* x, StateRef s, const float* w, const f
 // so it keeps the residual alone.
 template <bool R16>
 __global__ void __launch_bounds__(256) upsample_add_kernel(void* __restrict__ x10, const void* __restrict__ x5, int B,
-                                                           int T, int Tr, uint16_t* __restrict__ shadow, int64_t plane) {
+                                                           int T, int Tr, uint16_t* __restrict__ shadow, int64_t plane,
+                                                           float* __restrict__ xp) {
   // four consecutive channels per thread (8-byte fp16 / 16-byte fp32 residual vectors, 8-byte bf16 shadow)
   const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (idx >= (int64_t)B * T * kD) return;
@@ -682,6 +690,7 @@ __global__ void __launch_bounds__(256) upsample_add_kernel(void* __restrict__ x1
   f32x4_t v = load_res4(x10, idx, R16);
   if (t < 2 * Tr) v += load_res4(x5, (b * Tr + t / 2) * kD + c, R16);
   store_res4(x10, idx, v, R16);
+  if (!R16 && xp) *reinterpret_cast<f32x4_t*>(xp + xpk_off(row, c, kD)) = v;   // c % 4 == 0: one 16-byte run packed too
   if (shadow) {
     if (!plane) {
       const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
@@ -698,15 +707,16 @@ __global__ void __launch_bounds__(256) upsample_add_kernel(void* __restrict__ x1
 }
 
 hipError_t launch_upsample_add(void* x10, const void* x5, int B, int T, uint16_t* shadow, int64_t plane, bool r16,
-                               hipStream_t st) {
+                               hipStream_t st, float* xp) {
+  if (r16 && xp) return hipErrorInvalidValue;
   const int64_t n4 = (int64_t)B * T * kD / 4;
   const int Tr = (T + 1 - 3) / 2 + 1;
   if (r16)
     hipLaunchKernelGGL(upsample_add_kernel<true>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
-                       shadow, plane);
+                       shadow, plane, xp);
   else
     hipLaunchKernelGGL(upsample_add_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, x10, x5, B, T, Tr,
-                       shadow, plane);
+                       shadow, plane, xp);
   return hipGetLastError();
 }
 

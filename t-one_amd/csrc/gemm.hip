@@ -1018,7 +1018,13 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st) {
   }
   // fp32 split mode, fragment-packed operands (common.h xpk_off): the consumer is gemm_d3, the producer the fp32 SwiGLU
   // epilogue of gemm_x3 -- nothing else reads or writes that layout
-  if (a.a_packed) return bf16 ? hipErrorInvalidValue : gemm_d3(a, epi, -1, st);
+  if (a.a_packed) {
+    if (bf16) return hipErrorInvalidValue;
+    // the rowscale projections (FFN up, pw1, q|k|v) on the wide form, the N = 384 RESID / STORE ones on gemm_d3
+    if (a.rowscale || epi == EPI_SWIGLU || epi == EPI_GLU || a.N != kD) return gemm_d3n(a, epi, -1, st);
+    return gemm_d3(a, epi, -1, st);
+  }
+  if (a.CP) return hipErrorInvalidValue;   // the packed copy of C: written by the direct-load kernels only
   if (a.c_packed && (bf16 || epi != EPI_SWIGLU || !a.W3 || a.a_bf16 || a.c_bf16 || a.c_plane || a.M <= 64 ||
                      a.ldc % 32 != 0))
     return hipErrorInvalidValue;

@@ -168,6 +168,8 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
             o.w = rr[g].w + p.alpha * v[4 * g + 3];
             v[4 * g] = o.x; v[4 * g + 1] = o.y; v[4 * g + 2] = o.z; v[4 * g + 3] = o.w;
             if (ok) store_res4(p.C, mrow * p.ldc + nb + 8 * g + 4 * lh, o, R16);
+            // fp32: the packed copy the next rowscale projection reads (gemm_d3n; common.h xpk_off)
+            if (!R16 && p.CP && ok) *reinterpret_cast<f32x4*>(p.CP + xpk_off(mrow, nb + 8 * g + 4 * lh, (int)p.ldc)) = o;
           }
           if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
           else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);
@@ -178,6 +180,7 @@ __device__ __forceinline__ void tile_epilogue_inv(const GemmArgs& p, f32x16 (&ac
           for (int g = 0; g < 4; ++g) {
             const f32x4 o = {v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
             if (ok) store_res4(p.C, mrow * p.ldc + nb + 8 * g + 4 * lh, o, R16);   // fp32 or fp16 residual
+            if (!R16 && p.CP && ok) *reinterpret_cast<f32x4*>(p.CP + xpk_off(mrow, nb + 8 * g + 4 * lh, (int)p.ldc)) = o;
           }
           if (p.C2 && p.c2_plane) store_tile_split(p.C2 + mrow * p.ldc + nb, p.c2_plane, v, lh, ok);
           else if (p.C2) store_tile_bf16(p.C2 + mrow * p.ldc + nb, v, lh, ok);   // bf16 shadow (fp32 C)

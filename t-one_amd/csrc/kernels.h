@@ -19,6 +19,8 @@ struct Knobs {
                        // reciprocal per row instead of dividing each element (last-bit differences of the residual)
   int h_blocked;       // TONE_H_BLOCKED=0: the bf16 FFN hidden row-major instead of in 32 x 32 tiles (bit-identical)
   int ring_nt;         // TONE_RING_NT=0: dwconv_ring reads / writes the ring rows through the caches (bit-identical)
+  int d3x;             // TONE_D3X=0: fp32 pw1 on gemm_x3 instead of gemm_d3n over the packed copy of the residual rows that
+                       // attn-out writes (last-bit changes: the row factor's squares added in another order)
   int d3;              // TONE_D3=0: fp32 N = 384 projections at small M on gemm_x3 instead of gemm_d3 (last-bit changes:
                        // the K-split partials are added in another order)
 };
@@ -93,6 +95,7 @@ struct GemmArgs {
   // C written fragment-packed (the fp32 SWIGLU epilogue of gemm_x3, producing FFN down's A)
   const uint16_t* W3P;
   int a_packed, c_packed;
+  float* CP;           // fp32 STORE / RESID on gemm_d3: also C fragment-packed -- the next rowscale projection's A (gemm_d3n)
 };
 
 hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
@@ -102,6 +105,8 @@ hipError_t gemm(const GemmArgs& a, int epi, bool bf16, hipStream_t st);
 // its A written packed by the producer (a_packed) and W packed at load (W3P).
 hipError_t gemm_d3(const GemmArgs& a, int epi, int variant, hipStream_t st);
 bool gemm_d3_routed(int M, int K, int N);
+// the wide form (NT W tiles per wave, optional row factor; A packed or, SWIGLU only, row-major): experiments (variant)
+hipError_t gemm_d3n(const GemmArgs& a, int epi, int variant, hipStream_t st);
 // Row-panel residual GEMM (gemm_rp.hip): bf16 A / W, N = 384, the fp16 residual stream updated in place with the whole
 // output row per workgroup (optional fused RMSNorm, norm_w); bm = panel rows (0: about one panel per CU)
 hipError_t gemm_rp(const GemmArgs& a, hipStream_t st, int bm = 0);
@@ -227,8 +232,9 @@ hipError_t launch_sub1(const float* feats, StateRef s, const float* pre_norm_w, 
 // q8 / s8 / ss8 (fp8 mode, optional): also the MXFP8 form of the bf16 shadow row and its sum-of-squares slab,
 // exactly what launch_quant_mx would make from the shadow
 // r16: x is the bf16 / fp8 modes' fp16 residual stream (read and written as fp16)
+// xp (fp32 only): also the normalized rows fragment-packed (common.h xpk_off), the next FFN up's A on gemm_d3n
 hipError_t launch_rmsnorm(void* x, const float* w, int rows, uint16_t* shadow, int64_t plane, bool r16, hipStream_t st,
-                          uint8_t* q8 = nullptr, uint8_t* s8 = nullptr, float* ss8 = nullptr);
+                          uint8_t* q8 = nullptr, uint8_t* s8 = nullptr, float* ss8 = nullptr, float* xp = nullptr);
 
 // Layers 14/15: xn = RMSNorm(r); kv = [cache(S rows) ; xn]; next cache (left-padded to 30) -> state.
 // r is the residual stream: fp16 in the bf16 / fp8 modes (obf), fp32 in fp32 mode
@@ -268,12 +274,14 @@ hipError_t launch_ring_export(const __half* slab, int64_t sstride, const int* ro
                               __half* flat, int64_t fstride, int T, int Tr, int n, hipStream_t st);
 
 // a11: reduction state + grouped conv (384->1536, k3, s2) -> y [B*5][1536]; x fp16 (residual stream) when obf
+// y_packed (fp32 only): y fragment-packed (common.h xpk_off, ld 1536) for the 1x1 projection on gemm_d3
 hipError_t launch_reduce_conv(const void* x, StateRef s, const float* w, const float* b, void* y, bool obf, int B,
-                              int T, hipStream_t st);
+                              int T, hipStream_t st, bool y_packed = false);
 
 // a12: x10[b*10+t] += x5[b*5+t/2]; both fp16 (residual stream) when r16
+// xp (fp32 only): also the sum fragment-packed (common.h xpk_off), layer 15's FFN1 A on gemm_d3n
 hipError_t launch_upsample_add(void* x10, const void* x5, int B, int T, uint16_t* shadow, int64_t plane, bool r16,
-                               hipStream_t st);
+                               hipStream_t st, float* xp = nullptr);
 
 // a14: logits = x . Wd^T + bd, log_softmax over 35 classes -> logprobs [B*10][35]
 // a14 + decode flags: logprobs [rows][35]; optional frame_info[row] = greedy token | speech flag << 8

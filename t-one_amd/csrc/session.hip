@@ -35,6 +35,7 @@ const Knobs& knobs() {
     r.rp_norm = env("TONE_RP_NORM", 1) != 0;
     r.h_blocked = env("TONE_H_BLOCKED", 1) != 0;
     r.d3 = env("TONE_D3", 1) != 0;
+    r.d3x = env("TONE_D3X", 1) != 0;
     r.ring_nt = env("TONE_RING_NT", 1) != 0;
     return r;
   }();
@@ -127,6 +128,7 @@ struct tone_session {
   // activations
   float *wave, *power, *feats, *rA, *rB, *qkv, *kvp, *g, *probs;
   void *x2, *flat, *h, *ctx, *d, *xn, *kv, *yred;   // bf16 in bf16 mode
+  float *rAP = nullptr, *rBP = nullptr;   // fp32 mode: fragment-packed copies of rA / rB (gemm_d3n's A)
   uint16_t *xbA, *xbB;                              // bf16 shadows of rA / rB (bf16 mode)
   uint8_t *a8 = nullptr, *a8s = nullptr, *h8 = nullptr, *h8s = nullptr;   // fp8 mode: MXFP8 GEMM inputs
   float* ss8 = nullptr;                             // fp8 mode: sum-of-squares slab of a8's rows [rows][kSsSlots]
@@ -410,7 +412,8 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
               int64_t ldc, const float* bias, int M, int N, int K, int epi, int rowscale, const float* R = nullptr,
               float alpha = 1.0f, bool a_bf16 = false, bool c_bf16 = false, uint16_t* c2 = nullptr,
               bool mx_out = false, const DwFuse* dw = nullptr, const AttFuse* att = nullptr,
-              const float* norm_w = nullptr, bool h_blocked = false, bool a_packed = false, bool c_packed = false) {
+              const float* norm_w = nullptr, bool h_blocked = false, bool a_packed = false, bool c_packed = false,
+              float* cp = nullptr) {
   GemmArgs a{};   // value-initialised: every field not set below is zero
   a.norm_w = norm_w;
   a.h_blocked = h_blocked;
@@ -453,6 +456,7 @@ int gemm_call(tone_session* s, hipStream_t st, const char* fam, const void* A, i
   }
   a.a_packed = a_packed;
   a.c_packed = c_packed;
+  a.CP = cp;
   LAUNCH(fam, gemm(a, epi, bf, st));
   return TONE_OK;
 }
@@ -572,6 +576,13 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     const bool f32m = s->precision == TONE_PRECISION_FP32;
     const bool pk_h = f32m && gemm_d3_routed(M, kDff, D) && s->w3p.count(w.w2[0]) && s->w3p.count(w.w2[1]);
     const bool pk_d = f32m && gemm_d3_routed(M, D, D) && s->w3p.count(w.wo) && s->w3p.count(w.wpw2);
+    // ... and pw1 (GLU, folded norm) on gemm_d3n over a packed copy of the residual rows that attn-out writes beside them
+    // (GemmArgs::CP): 217 vs 267 us per fp32 B = 256 step.  FFN up and q|k|v on gemm_d3n measured no faster in the step
+    // (1039 vs 1019, 163 vs 160 us: their 7 / 2.6 MB of packed W planes come cold from HBM each layer, where gemm_x3 keeps
+    // its W tile in LDS across row blocks; profiles/r06_d3x_all_ab.jsonl, step_r06_d3x_all_fp32_b256.txt; pw1 alone: r06_d3x_pw1_ab.jsonl) and the packed copies
+    // they need cost their writes, so they stay on gemm_x3
+    const bool pk_pw1 = pk_d && knobs().d3x && s->w3p.count(w.wpw1);
+    float* xp = pk_pw1 ? (x == s->rA ? s->rAP : s->rBP) : nullptr;
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
     // fp8 mode: the residual shadow quantized to MXFP8 (with its row factor), h produced as MXFP8 by the
     // up-projection's epilogue
@@ -665,7 +676,7 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       aa.ctx_packed = pk_d;
       LAUNCH("attention", launch_attention(aa, st));
       CALL(gemm_call(s, st, "gemm_attn_out", s->ctx, D, w.wo, x, D, w.bo, M, D, D, EPI_RESID, 0, x, 1.0f, true, false,
-                     xs, false, nullptr, nullptr, nullptr, false, pk_d));
+                     xs, false, nullptr, nullptr, nullptr, false, pk_d, false, xp));
     }
     q8_fresh = false;
     // Convolution module (conformer_blocks.py:827-830)
@@ -676,8 +687,9 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
       CALL(gemm_call(s, st, "gemm_pw1_dwconv", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f,
                      false, false, nullptr, false, &dw));
     } else {
-      CALL(gemm_call(s, st, "gemm_pw1", xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D, D, EPI_GLU, 1, nullptr, 1.0f, true,
-                     true));   // g in bf16 in the bf16 / fp8 modes (fp32 in fp32 mode: gemm_call drops c_bf16 there)
+      CALL(gemm_call(s, st, "gemm_pw1", pk_pw1 ? static_cast<const void*>(xp) : xa, D, w.wpw1, s->g, D, w.bpw1, M, 2 * D,
+                     D, EPI_GLU, 1, nullptr, 1.0f, true, true, nullptr, false, nullptr, nullptr, nullptr, false, pk_pw1));
+      // (g in bf16 in the bf16 / fp8 modes; fp32 in fp32 mode: gemm_call drops c_bf16 there)
       LAUNCH("dwconv", launch_dwconv(s->g, sr, l, w.wdw, w.bdw, s->d, bf, T, B, st, pk_d));
     }
     // fp8 mode: pw2 also emits FFN2's MXFP8 operand
@@ -695,9 +707,12 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     if (!norm_fused)
       LAUNCH("norm", launch_rmsnorm(x, w.norm_out, M, xs, 0, bf, st, q8_fresh ? s->a8 : nullptr, s->a8s, s->ss8));
     if (l == 6) {  // CausalTemporalReduction (conformer.py:221-222); rA keeps the residual
-      LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, geo.T, st));
+      // fp32 mode: the 1x1 (K = 1536, N = 384) on gemm_d3 over y written packed by reduce_conv
+      const bool pk_y = s->precision == TONE_PRECISION_FP32 && gemm_d3_routed(B * geo.Tr, 4 * D, D) &&
+                        s->w3p.count(s->wred_pw);
+      LAUNCH("reduce_conv", launch_reduce_conv(s->rA, sr, s->wred, s->bred, s->yred, bf, B, geo.T, st, pk_y));
       CALL(gemm_call(s, st, "gemm_reduce", s->yred, 4 * D, s->wred_pw, s->rB, D, s->bred_pw, B * geo.Tr, D, 4 * D,
-                     EPI_STORE, 0, nullptr, 1.0f, true, false, shB));
+                     EPI_STORE, 0, nullptr, 1.0f, true, false, shB, false, nullptr, nullptr, nullptr, false, pk_y));
       x = s->rB;
       xs = shB;
       T = geo.Tr;
@@ -827,7 +842,7 @@ int finalize_weights(tone_session* s) {
   CALL(upload(s, &s->out_norm, *outn));
   CALL(upload(s, &s->wred, *rw));
   CALL(upload(s, &s->bred, *rb));
-  CALL(upload_w(s, &s->wred_pw, *rpw));
+  CALL(upload_w(s, &s->wred_pw, *rpw, 4 * kD));
   CALL(upload(s, &s->bred_pw, *rpb));
   CALL(upload(s, &s->whead, *hw));
   CALL(upload(s, &s->bhead, *hb));
@@ -944,7 +959,7 @@ int finalize_weights(tone_session* s) {
         bp[64 * q + r] = (*pb1)[src];
         bp[64 * q + 32 + r] = (*pb1)[D + src];
       }
-    CALL(upload_w(s, &lw.wpw1, wp));
+    CALL(upload_w(s, &lw.wpw1, wp, kD));
     CALL(upload(s, &lw.bpw1, bp));
     std::vector<float> wd((size_t)D * kConvK), bd(D);
     for (int ch = 0; ch < D; ++ch) {
@@ -979,7 +994,11 @@ int finalize_weights(tone_session* s) {
   CALL(dalloc(s, &s->g, MB * kTMax * D));
   CALL(dalloc(s, reinterpret_cast<float**>(&s->d), (MB * kTMax + 32) * D));
   CALL(dalloc(s, &s->probs, MB * kHeads * kTMax * (30 + kTMax)));
-  CALL(dalloc(s, reinterpret_cast<float**>(&s->yred), MB * kTrMax * 4 * D));
+  CALL(dalloc(s, reinterpret_cast<float**>(&s->yred), (MB * kTrMax + 32) * 4 * D));   // + 32 rows: packed form
+  if (s->precision == TONE_PRECISION_FP32) {
+    CALL(dalloc(s, &s->rAP, (MB * kTMax + 32) * D));
+    CALL(dalloc(s, &s->rBP, (MB * kTrMax + 32) * D));
+  }
   CALL(dalloc(s, &s->xbA, MB * kTMax * D));
   CALL(dalloc(s, &s->xbB, MB * kTrMax * D));
   if (s->precision == TONE_PRECISION_FP8) {

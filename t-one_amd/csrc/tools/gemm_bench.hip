@@ -439,7 +439,12 @@ int main(int argc, char** argv) {
     // for the check)
     a.a_packed = vv <= -499 && getenv("PACKX") && atoi(getenv("PACKX"));   // -499: gemm()'s routing (gemm_d3 by shape)
     if (a.a_packed) a.A = Afp;
-    a.c_packed = f32 && epi == 2 && vv > -300 && getenv("CPACK") && atoi(getenv("CPACK"));
+    a.c_packed = f32 && epi == 2 && (vv > -300 || vv == -499) && getenv("CPACK") && atoi(getenv("CPACK"));
+    // CPOUT=1 (gemm_d3 STORE / RESID through gemm()): also the packed copy of C (GemmArgs::CP), checked unpacked
+    const bool cpout = vv == -499 && (epi == 0 || epi == 1) && getenv("CPOUT") && atoi(getenv("CPOUT"));
+    static float* CPbuf = nullptr;
+    if (cpout && !CPbuf) CK(hipMalloc(&CPbuf, ((size_t)M + 32) * nout * 4));
+    a.CP = cpout ? CPbuf : nullptr;
     a.W = f32 ? (const void*)Wf : (const void*)W;
     a.a_bf16 = !f32;
     a.c_bf16 = f32 ? 0 : cbf;
@@ -473,7 +478,8 @@ int main(int argc, char** argv) {
       a.C8 = nullptr; a.C8s = nullptr; a.ss8 = nullptr;
     }
     auto launch = [&]() {
-      return vv <= -500 ? gemm_d3(a, epi, -500 - vv, 0)   // -500 - c: gemm_d3 variant c
+      return vv <= -600 ? gemm_d3n(a, epi, -600 - vv, 0)   // -600 - c: gemm_d3n variant c
+             : vv <= -500 ? gemm_d3(a, epi, -500 - vv, 0)   // -500 - c: gemm_d3 variant c
              : vv == -499 ? gemm(a, epi, false, 0)
              : vv <= -300 ? gemm_xw(a, epi, -300 - vv, 0)   // -300: gemm_xw auto run length, -300 - c: c W tiles per item
              : v < 0 ? gemm(a, epi, !f32, 0)
@@ -504,6 +510,16 @@ int main(int argc, char** argv) {
                          static_cast<const uint16_t*>(C), Cun, (int64_t)M, nout, 0);
       Cchk = Cun;
     }
+    float cp_err = -1.f;
+    if (cpout) {   // the packed copy, unpacked, against the same reference
+      if (!Cunf) CK(hipMalloc(&Cunf, (size_t)M * nout * 4));
+      hipLaunchKernelGGL(xunpack_kernel, dim3((unsigned)(((int64_t)M * nout + 255) / 256)), dim3(256), 0, 0, CPbuf, Cunf,
+                         (int64_t)M, nout);
+      CK(hipMemset(err, 0, 4));
+      hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, (const void*)Cunf, 0, chk_ref, (int64_t)M * nout, err);
+      CK(hipMemcpy(&cp_err, err, 4, hipMemcpyDeviceToHost));
+      CK(hipMemset(err, 0, 4));
+    }
     hipLaunchKernelGGL(err_kernel, dim3(1024), dim3(256), 0, 0, Cchk, a.res16 && epi <= 1 ? 2 : a.c_bf16, chk_ref, (int64_t)M * nout, err);
     float herr, herr2 = 0.f, q8_inv_err = 0.f;
     int q8_bad = -1;
@@ -522,9 +538,9 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
-    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"shadow_err\": %.3g, \"norm\": %d, \"q8_bad\": %d, \"q8_inv_err\": %.3g, \"hblk\": %d}\n",
+    printf("{\"M\": %d, \"K\": %d, \"N\": %d, \"epi\": %d, \"variant\": %d, \"nsplit\": %d, \"us\": %.2f, \"tflops\": %.1f, \"max_rel_err\": %.3g, \"shadow_err\": %.3g, \"norm\": %d, \"q8_bad\": %d, \"q8_inv_err\": %.3g, \"hblk\": %d, \"cp_err\": %.3g}\n",
            M, K, N, epi, vv, nsplit, us, flop / us * 1e-6, herr, herr2, a.norm_w && epi == 1 ? 1 : 0, q8_bad, q8_inv_err,
-           (int)hblk);
+           (int)hblk, cp_err);
     fflush(stdout);
   }
   return 0;

@@ -550,10 +550,10 @@ __global__ void xunpack_kernel(const float* src, float* dst, int64_t rows, int l
   if (i >= rows * ld) return;
   dst[i] = src[xpk_off(i / ld, (int)(i % ld), ld)];
 }
-static const void* unpacked(const void* out, int64_t rows) {
-  if (!g_pk) return out;
-  float* u = pool.get<float>(rows * kD);
-  hipLaunchKernelGGL(xunpack_kernel, grid1(rows * kD), dim3(256), 0, 0, static_cast<const float*>(out), u, rows, kD);
+static const void* unpacked(const void* out, int64_t rows, int ld = kD, bool force = false) {
+  if (!g_pk && !force) return out;
+  float* u = pool.get<float>(rows * ld);
+  hipLaunchKernelGGL(xunpack_kernel, grid1(rows * ld), dim3(256), 0, 0, static_cast<const float*>(out), u, rows, ld);
   CK(hipDeviceSynchronize());
   return u;
 }
@@ -974,7 +974,7 @@ static void check_reduce(int B, int T, bool bf, Report& rep) {
   const void* x = bf ? (const void*)to_f16(xf, M * kD) : (const void*)xf;
   const float* w = rand_f32(4 * kD * 3, 62, 0.3f);
   const float* bias = rand_f32(4 * kD, 63, 0.2f);
-  void* y = bf ? (void*)pool.get<uint16_t>((int64_t)B * TR * 4 * kD) : (void*)pool.get<float>((int64_t)B * TR * 4 * kD);
+  void* y = bf ? (void*)pool.get<uint16_t>((int64_t)B * TR * 4 * kD) : (void*)pool.get<float>(((int64_t)B * TR + 32) * 4 * kD);
   float* yr = pool.get<float>((int64_t)B * TR * 4 * kD);
   Secs secs{};
   secs.s[0] = {kOffRed, kD};
@@ -984,8 +984,9 @@ static void check_reduce(int B, int T, bool bf, Report& rep) {
   hipLaunchKernelGGL(ref_reduce_kernel, grid1((int64_t)B * 4 * kD), dim3(256), 0, 0, x, bf ? 2 : 0, sl.ref(), w, bias, T, yr,
                      exps, B);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([=] { return launch_reduce_conv(x, sl.ref(), w, bias, y, bf, B, T, 0); });
-  rep.out("y", y, bf ? 1 : 0, 4 * kD, yr, (int64_t)B * TR, 4 * kD);
+  const bool pk = g_pk;
+  rep.us = time_once([=] { return launch_reduce_conv(x, sl.ref(), w, bias, y, bf, B, T, 0, pk); });
+  rep.out("y", unpacked(y, (int64_t)B * TR, 4 * kD), bf ? 1 : 0, 4 * kD, yr, (int64_t)B * TR, 4 * kD);
   rep.state(sl, secs, exps);
 }
 
@@ -1019,9 +1020,11 @@ static void check_upsample(int B, int T, bool r16, Report& rep) {
   const void* x5 = r16 ? (const void*)to_f16(c, n5) : (const void*)c;
   uint16_t* shadow = pool.get<uint16_t>(n10);
   CK(hipDeviceSynchronize());
-  rep.us = time_once([=] { return launch_upsample_add(x10, x5, B, T, shadow, 0, r16, 0); });
+  float* xp = g_pk ? pool.get<float>(((int64_t)B * T + 32) * kD) : nullptr;
+  rep.us = time_once([=] { return launch_upsample_add(x10, x5, B, T, shadow, 0, r16, 0, xp); });
   rep.out("x", x10, r16 ? 2 : 0, kD, ref, (int64_t)B * T, kD);
   rep.out("shadow", shadow, 1, kD, ref, (int64_t)B * T, kD);
+  if (xp) rep.out("xp", unpacked(xp, (int64_t)B * T), 0, kD, ref, (int64_t)B * T, kD);
 }
 
 // =====================================================================================================================
@@ -1127,8 +1130,10 @@ static void check_rmsnorm(int rows, bool r16, bool q8, Report& rep) {
     ss = pool.get<float>((int64_t)rows * kSsSlots);
   }
   CK(hipDeviceSynchronize());
-  rep.us = time_once([=] { return launch_rmsnorm(x, w, rows, shadow, 0, r16, 0, q, s, ss); });
+  float* xp = g_pk ? pool.get<float>(((int64_t)rows + 32) * kD) : nullptr;
+  rep.us = time_once([=] { return launch_rmsnorm(x, w, rows, shadow, 0, r16, 0, q, s, ss, xp); });
   rep.out("x", x, r16 ? 2 : 0, kD, ref, rows, kD);
+  if (xp) rep.out("xp", unpacked(xp, rows), 0, kD, ref, rows, kD);
   rep.out("shadow", shadow, 1, kD, ref, rows, kD);
   if (q8) {
     uint8_t* q2 = pool.get<uint8_t>(n);
@@ -1158,8 +1163,8 @@ int main(int argc, char** argv) {
     fprintf(stderr,
             "usage: %s <check> <B> [T]\n  checks: sub_conv sub1_f32 sub1_f32_400 sub1_bf16_400 conv2_f32 conv2_f32_400 "
             "conv2_bf16_400 dwconv[_bf16|_pk] dwconv_ring[_bf16|_pk] attn_rec[_bf16|_pk] (T S) attn_shared[_bf16|_pk] "
-            "kv[_bf16] (T S) kv_ring[_bf16] (T S) reduce[_bf16] "
-            "upsample[_r16] head[_r16] (rows) rmsnorm[_r16|_q8] (rows)\n",
+            "kv[_bf16] (T S) kv_ring[_bf16] (T S) reduce[_bf16|_pk] "
+            "upsample[_r16|_pk] head[_r16] (rows) rmsnorm[_r16|_q8|_pk] (rows)\n",
             argv[0]);
     return 2;
   }

@@ -144,10 +144,22 @@ def test_fp32_routes_match_reference(M, K, N, epi, rs):
 # last 32-row block NaN, so a read of them that reached an output would show), through gemm()'s own routing, full fp32
 # operands against fp64
 @pytest.mark.parametrize("M", [2560, 1280, 3328, 1536, 640, 320, 100])
-@pytest.mark.parametrize("K", [384, 1536])
-def test_fp32_d3_packed_matches_reference(M, K):
+@pytest.mark.parametrize("K,epi", [(384, 1), (1536, 1), (1536, 0)])
+def test_fp32_d3_packed_matches_reference(M, K, epi):
+    """... RESID (attn-out, pw2, FFN down) and STORE (the reduction's 1x1, K = 1536), with the packed copy of C that the
+    next rowscale projection reads (GemmArgs::CP) checked through the inverse map."""
     _gpu()
-    r = _run(M, K, 384, 1, -499, {"FULLF32": 1, "NOC2": 1, "PACKX": 1})
+    r = _run(M, K, 384, epi, -499, {"FULLF32": 1, "NOC2": 1, "PACKX": 1, "CPOUT": 1})
+    assert r["max_rel_err"] < 2e-5 and 0 <= r["cp_err"] < 2e-5, r
+
+
+# the rowscale projections on gemm_d3n over the packed copy of the residual stream (folded-norm row factor from the
+# packed rows): FFN up (SwiGLU, h written packed for FFN down), pw1 (GLU), q|k|v (layers 0 / 7), v (the shared layers)
+@pytest.mark.parametrize("M", [2560, 1280, 3328, 1536, 640, 100])
+@pytest.mark.parametrize("N,epi,cpack", [(3072, 2, 1), (768, 3, 0), (1152, 0, 0), (384, 0, 0)])
+def test_fp32_d3n_rowscale_matches_reference(M, N, epi, cpack):
+    _gpu()
+    r = _run(M, 384, N, epi, -499, {"FULLF32": 1, "NOC2": 1, "PACKX": 1, "ROWSCALE": 1, "CPACK": cpack})
     assert r["max_rel_err"] < 2e-5, r
 
 
@@ -312,7 +324,8 @@ def test_kv_assemble_ring_every_element(T, S, check, B, tol):
 
 
 @pytest.mark.parametrize("T", [10, 13])
-@pytest.mark.parametrize("check,B,tol", [("reduce_bf16", 4096, 1e-2), ("reduce", 256, 1e-5)])
+@pytest.mark.parametrize("check,B,tol", [("reduce_bf16", 4096, 1e-2), ("reduce", 256, 1e-5), ("reduce_pk", 256, 1e-5),
+                                         ("reduce_pk", 13, 1e-5)])
 def test_reduce_conv_every_element(T, check, B, tol):
     _gpu()
     r = _check(check, B, T)
@@ -321,11 +334,14 @@ def test_reduce_conv_every_element(T, check, B, tol):
 
 
 @pytest.mark.parametrize("T", [10, 13])
-@pytest.mark.parametrize("check,B,tol", [("upsample_r16", 4096, 2e-3), ("upsample", 256, 1e-6)])
+@pytest.mark.parametrize("check,B,tol", [("upsample_r16", 4096, 2e-3), ("upsample", 256, 1e-6), ("upsample_pk", 256, 1e-6)])
 def test_upsample_add_every_element(T, check, B, tol):
+    """... "_pk": also the packed copy of the sum (layer 15's FFN1 A on gemm_d3n)."""
     _gpu()
     r = _check(check, B, T)
     assert r["outputs"]["x"] < tol and r["outputs"]["shadow"] < 1e-2, r
+    if check.endswith("_pk"):
+        assert r["outputs"]["xp"] < tol, r
 
 
 @pytest.mark.parametrize("check,rows", [("head_r16", 40960), ("head_r16", 20480), ("head", 2560), ("head", 60),
@@ -338,10 +354,12 @@ def test_head_every_element(check, rows):
 
 
 @pytest.mark.parametrize("check,rows,tol", [("rmsnorm_q8", 40960, 2e-3), ("rmsnorm_r16", 20480, 2e-3),
-                                            ("rmsnorm", 2560, 1e-5)])
+                                            ("rmsnorm", 2560, 1e-5), ("rmsnorm_pk", 2560, 1e-5), ("rmsnorm_pk", 100, 1e-5)])
 def test_rmsnorm_every_element(check, rows, tol):
     _gpu()
     r = _check(check, rows)
     assert r["outputs"]["x"] < tol and r["outputs"]["shadow"] < 1e-2, r
+    if check.endswith("_pk"):   # the packed copy (the next FFN up's A on gemm_d3n)
+        assert r["outputs"]["xp"] < tol, r
     if "q8_bad_bytes" in r["outputs"]:
         assert r["outputs"]["q8_bad_bytes"] == 0 and r["outputs"]["q8_row_factor"] < 1e-5, r
