@@ -4,7 +4,7 @@
 set -u
 out=gpurun_out/${1:-d3n}_sweep.jsonl
 mkdir -p gpurun_out; : > $out
-V=-2,-600,-601,-602,-603,-604,-605
+V=-2,-602,-603
 for M in 2560 1280; do
   for NE in "3072 2" "768 3" "1152 0"; do
     set -- $NE

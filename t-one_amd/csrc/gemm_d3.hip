@@ -240,13 +240,10 @@ hipError_t launch_d3n_e(const GemmArgs& a, hipStream_t st) {
 template <int WM, int WN, int NT, int D>
 hipError_t launch_d3n(const GemmArgs& a, int epi, hipStream_t st) {
   if (a.N % (32 * WN * NT) != 0 || (a.K / 32) % D != 0) return hipErrorInvalidValue;
-  if (a.a_packed) {
-    if (epi == EPI_SWIGLU) return launch_d3n_e<WM, WN, NT, D, EPI_SWIGLU, true>(a, st);
-    if (epi == EPI_GLU) return launch_d3n_e<WM, WN, NT, D, EPI_GLU, true>(a, st);
-    if (epi == EPI_STORE) return launch_d3n_e<WM, WN, NT, D, EPI_STORE, true>(a, st);
-  } else {
-    if (epi == EPI_SWIGLU) return launch_d3n_e<WM, WN, NT, D, EPI_SWIGLU, false>(a, st);
-  }
+  if (!a.a_packed) return hipErrorInvalidValue;   // row-major A: ~5 % ahead of gemm_x3 at best, not kept
+  if (epi == EPI_SWIGLU) return launch_d3n_e<WM, WN, NT, D, EPI_SWIGLU, true>(a, st);
+  if (epi == EPI_GLU) return launch_d3n_e<WM, WN, NT, D, EPI_GLU, true>(a, st);
+  if (epi == EPI_STORE) return launch_d3n_e<WM, WN, NT, D, EPI_STORE, true>(a, st);
   return hipErrorInvalidValue;
 }
 
@@ -312,17 +309,13 @@ hipError_t gemm_d3n(const GemmArgs& a, int epi, int variant, hipStream_t st) {
       a.norm_w || a.h_blocked || (a.c_packed && epi != EPI_SWIGLU) || a.K % 32 != 0 || a.lda % 4 != 0 ||
       a.ldc % 4 != 0 || a.M <= 0 || (a.a_packed && a.lda != a.K))
     return hipErrorInvalidValue;
-  // by shape (scripts/d3n_sweep.sh, profiles/r06_d3n_packed_sweep.jsonl, A packed, K = 384; in the step only pw1 gains, session.hip): four W tiles per wave over four
-  // row blocks (3) for FFN up (M = 2560 / 1280: 43.2 / 23.8 vs 49.0 / 26.9 us on gemm_x3) and q|k|v at M >= 2048 (21.4 vs
+  // by shape (scripts/d3n_sweep.sh, profiles/r06_d3n_packed_sweep.jsonl, A packed, K = 384; in the step only pw1
+  // gains, session.hip): four W tiles per wave over four row blocks (3) for FFN up (M = 2560 / 1280: 43.2 / 23.8 vs 49.0 / 26.9 us on gemm_x3) and q|k|v at M >= 2048 (21.4 vs
   // 24.9); two (2) for pw1 (14.6 / 13.0 vs 17.2 / 14.8) and the rest (q|k|v at 1280: 13.7 vs 15.7)
   if (variant < 0) variant = (epi == EPI_SWIGLU || (a.N >= 1024 && a.M >= 2048)) ? 3 : 2;
-  switch (variant) {
-    case 0: return launch_d3n<2, 2, 2, 3>(a, epi, st);
-    case 1: return launch_d3n<2, 2, 4, 2>(a, epi, st);
+  switch (variant) {   // the sweep's other arrangements (2 x 2 / 1 x 4 waves) were slower on every shape
     case 2: return launch_d3n<4, 1, 2, 3>(a, epi, st);
     case 3: return launch_d3n<4, 1, 4, 2>(a, epi, st);
-    case 4: return launch_d3n<1, 4, 2, 3>(a, epi, st);
-    case 5: return launch_d3n<1, 4, 4, 2>(a, epi, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -579,8 +579,8 @@ int enqueue_step(tone_session* s, const int32_t* signal, StateRef sr, float* log
     // ... and pw1 (GLU, folded norm) on gemm_d3n over a packed copy of the residual rows that attn-out writes beside them
     // (GemmArgs::CP): 217 vs 267 us per fp32 B = 256 step.  FFN up and q|k|v on gemm_d3n measured no faster in the step
     // (1039 vs 1019, 163 vs 160 us: their 7 / 2.6 MB of packed W planes come cold from HBM each layer, where gemm_x3 keeps
-    // its W tile in LDS across row blocks; profiles/r06_d3x_all_ab.jsonl, step_r06_d3x_all_fp32_b256.txt; pw1 alone: r06_d3x_pw1_ab.jsonl) and the packed copies
-    // they need cost their writes, so they stay on gemm_x3
+    // its W tile in LDS across row blocks; profiles/r06_d3x_all_ab.jsonl, step_r06_d3x_all_fp32_b256.txt; pw1 alone:
+    // r06_d3x_pw1_ab.jsonl) and the packed copies they need cost their writes, so they stay on gemm_x3
     const bool pk_pw1 = pk_d && knobs().d3x && s->w3p.count(w.wpw1);
     float* xp = pk_pw1 ? (x == s->rA ? s->rAP : s->rBP) : nullptr;
     // FFN1 (conformer_blocks.py:812-814); h in bf16 in bf16 mode
