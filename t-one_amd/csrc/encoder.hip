@@ -651,12 +651,26 @@ __global__ void __launch_bounds__(256) reduce_conv_kernel(const void* __restrict
   xc[0] = __half2float(s.in[s.row_in(b) + kOffRed + c]);
   for (int t = 0; t < T; ++t) xc[t + 1] = load_res<OBF>(x, ((int64_t)b * T + t) * kD + c);   // fp16 residual when OBF
   s.out[s.row_out(b) + kOffRed + c] = __float2half_rn(xc[T]);
+  if (!OBF && ypk) {   // packed y (gemm_d3's A): the 4 outputs of this channel are one 16-byte run there too
+    float wq[4][3], bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = 4 * c + q;
+      wq[q][0] = w[o * 3]; wq[q][1] = w[o * 3 + 1]; wq[q][2] = w[o * 3 + 2]; bq[q] = bias[o];
+    }
+    for (int t = 0; t < TR; ++t) {
+      f32x4_t v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = bq[q] + wq[q][0] * xc[2 * t] + wq[q][1] * xc[2 * t + 1] + wq[q][2] * xc[2 * t + 2];
+      *reinterpret_cast<f32x4_t*>(static_cast<float*>(y) + xpk_off((int64_t)b * TR + t, 4 * c, 4 * kD)) = v;
+    }
+    return;
+  }
   for (int q = 0; q < 4; ++q) {
     const int o = 4 * c + q;
     const float w0 = w[o * 3], w1 = w[o * 3 + 1], w2 = w[o * 3 + 2], bo = bias[o];
     for (int t = 0; t < TR; ++t)
-      store_act<OBF>(y, act_off((int64_t)b * TR + t, o, 4 * kD, !OBF && ypk),
-                     bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2]);
+      store_act<OBF>(y, ((int64_t)b * TR + t) * (4 * kD) + o, bo + w0 * xc[2 * t] + w1 * xc[2 * t + 1] + w2 * xc[2 * t + 2]);
   }
 }
 
