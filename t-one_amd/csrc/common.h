@@ -117,10 +117,23 @@ struct StateRef {
 };
 
 // MXFP8 (OCP MX, e4m3 values, one E8M0 scale per 32): the block exponent from the block's max |v|,
-// E = floor(log2 amax) - 8 (biased by 127, clamped), and the inverse block scale 2^(127 - E)
+// E = floor(log2 amax) - 7 (biased by 127, clamped to 1 .. 254), and the inverse block scale 2^(127 - E).  Round 6: one
+// binade of headroom below the OCP choice (- 8): the scaled values stay below 256 < 448, so no saturation can occur and
+// gfx950's scaled conversion (v_cvt_scalef32_pk_fp8_f32: cvt(x / 2^(E - 127)), which does not saturate) encodes a block
+// in one instruction per two values instead of a multiply, two clamps and a conversion; the lowest binade of e4m3
+// (values below 2^-15 of the block max) is what the headroom costs.  Weights keep the OCP exponent (host, once).
 __device__ __forceinline__ int mx_exp(float amax) {
   const int e = (int)((__float_as_uint(amax) >> 23) & 0xff);   // biased exponent of amax (0 for 0/subnormal)
-  return max(0, min(254, e - 8));
+  return max(1, min(254, e - 7));
+}
+// the block scale 2^(E - 127) as the float operand of the scaled conversion (E >= 1: a normal float)
+__device__ __forceinline__ float mx_scale(int ebiased) { return __uint_as_float((uint32_t)ebiased << 23); }
+typedef short mx_s16x2 __attribute__((ext_vector_type(2)));
+// two floats -> two e4m3 bytes of x / 2^(E - 127) in the low (HI false) or high half of w; NaN stays NaN
+template <bool HI>
+__device__ __forceinline__ uint32_t mx_cvt2(float a, float b, float scale, uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(__builtin_bit_cast(mx_s16x2, w), a, b,
+                                                                               scale, HI));
 }
 // clamp to e4m3's finite range (+-448) keeping a NaN a NaN: IEEE 754-2019 maximum / minimum (v_maximum3_f32 /
 // v_minimum3_f32 on gfx950) propagate NaN, so two instructions do what fminf / fmaxf plus a NaN select did in four
@@ -145,10 +158,10 @@ __device__ __forceinline__ float mx_row_inv(const float* __restrict__ ss_row) {
   const float ss = (((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w))) + ((c.x + c.y) + (c.z + c.w));
   return 1.0f / (sqrtf(ss) * 0.05103103630798288f + kRmsEps);   // 384^-0.5
 }
-// 4 floats -> 4 e4m3 bytes (one dword) with the block's inverse scale, saturating, NaN kept
-__device__ __forceinline__ uint32_t quant4(float a, float b, float c, float d, float inv) {
-  uint32_t w = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(a * inv), sat_e4m3(b * inv), 0, false);
-  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(c * inv), sat_e4m3(d * inv), (int)w, true);
+// 4 floats -> 4 e4m3 bytes (one dword) of the block with biased exponent e (mx_exp), NaN kept
+__device__ __forceinline__ uint32_t quant4(float a, float b, float c, float d, int e) {
+  const float sc = mx_scale(e);
+  return mx_cvt2<true>(c, d, sc, mx_cvt2<false>(a, b, sc, 0u));
 }
 
 // One 1 KiB LDS-DMA piece (global_load_lds_dwordx4: lane l's 16 bytes at src land at lds_dst + 16 l) issued from

@@ -47,8 +47,7 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(void* __restrict__ x, cons
 #pragma unroll
       for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
       const int e = mx_exp(am);
-      const float a = sat_e4m3(vb * exp2i(e));
-      q8[(int64_t)row * kD + lane + 64 * i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(a, 0.f, 0, false) & 0xff);
+      q8[(int64_t)row * kD + lane + 64 * i] = (uint8_t)(mx_cvt2<false>(vb, 0.f, mx_scale(e), 0u) & 0xff);
       if ((lane & 31) == 0) s8[(int64_t)row * (kD / 32) + 2 * i + (lane >> 5)] = (uint8_t)e;
     }
   }

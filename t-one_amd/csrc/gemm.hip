@@ -288,7 +288,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, f32x16 (&ac
         am = fmaxf(am, __shfl_xor(am, 2, 64));
         am = fmaxf(am, __shfl_xor(am, 4, 64));
         const int e = mx_exp(am);
-        const uint32_t q4 = quant4(b0, b1, b2, b3, exp2i(e));
+        const uint32_t q4 = quant4(b0, b1, b2, b3, e);
         float ssq = fmaf(b3, b3, fmaf(b2, b2, fmaf(b1, b1, b0 * b0)));
 #pragma unroll
         for (int w = 1; w < 32; w <<= 1) ssq += __shfl_xor(ssq, w, 64);

@@ -39,20 +39,14 @@ __device__ __forceinline__ float fsig(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
 
-// v / 2^(E - 127) clamped to e4m3's range, two values packed into the low / high half of `w`; a NaN stays a
-// NaN (the conversion encodes it as e4m3 NaN) instead of being clamped to a finite value
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <bool HI>
-__device__ __forceinline__ uint32_t cvt_pk(float a, float b, float inv, uint32_t w) {
-  const f32x2 p = f32x2{a, b} * inv;                         // one v_pk_mul_f32
-  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(p.x), sat_e4m3(p.y), (int)w, HI);
-}
-// 8 floats -> 8 e4m3 bytes with the block's inverse scale
-__device__ __forceinline__ u32x2 quant8(const float (&v)[8], float inv) {
-  uint32_t w0 = cvt_pk<false>(v[0], v[1], inv, 0u);
-  w0 = cvt_pk<true>(v[2], v[3], inv, w0);
-  uint32_t w1 = cvt_pk<false>(v[4], v[5], inv, 0u);
-  w1 = cvt_pk<true>(v[6], v[7], inv, w1);
+// 8 floats -> 8 e4m3 bytes of the block with biased exponent e (common.h mx_exp / mx_cvt2: the scaled conversion, no
+// saturation needed with the exponent's headroom; a NaN stays a NaN)
+__device__ __forceinline__ u32x2 quant8(const float (&v)[8], int e) {
+  const float sc = mx_scale(e);
+  uint32_t w0 = mx_cvt2<false>(v[0], v[1], sc, 0u);
+  w0 = mx_cvt2<true>(v[2], v[3], sc, w0);
+  uint32_t w1 = mx_cvt2<false>(v[4], v[5], sc, 0u);
+  w1 = mx_cvt2<true>(v[6], v[7], sc, w1);
   return u32x2{w0, w1};
 }
 
@@ -88,7 +82,7 @@ __global__ void __launch_bounds__(256) quant_mx_kernel(const uint16_t* __restric
     am = fmaxf(am, __shfl_xor(am, 1, 64));
     am = fmaxf(am, __shfl_xor(am, 2, 64));
     const int e = mx_exp(am);
-    const u32x2 q = quant8(v, exp2i(e));
+    const u32x2 q = quant8(v, e);
     if (on) {
       *reinterpret_cast<u32x2*>(Q + (int64_t)row * K + 8 * c) = q;
       if ((c & 3) == 0) S[(int64_t)row * (K / 32) + c / 4] = (uint8_t)e;
@@ -277,7 +271,7 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
           for (int r = 0; r < 8; ++r) am = fmaxf(am, fabsf(v[r]));
           am = lg_max(am);
           const int e = mx_exp(am);
-          const u32x2 qv = quant8(v, exp2i(e));
+          const u32x2 qv = quant8(v, e);
           const int blk = (n0 >> 1) + (wrow0 >> 1) + 32 * pb;     // first output column of the block
           if (ok) {
             *reinterpret_cast<u32x2*>(p.C8 + mrow * p.ldc + blk + 16 * (lg & 1) + 8 * (lg >> 1)) = qv;
@@ -331,11 +325,10 @@ __global__ void __launch_bounds__(512) gemm_mx_kernel(MxArgs p) {
                 }
               am = lg_max(am);
               const int e = mx_exp(am);
-              const float sc = exp2i(e);
               const int col = n0 + wrow0 + 32 * k + 4 * lg;
 #pragma unroll
               for (int h = 0; h < 2; ++h) {
-                const uint32_t q4 = quant4(vq[2 * k + h][0], vq[2 * k + h][1], vq[2 * k + h][2], vq[2 * k + h][3], sc);
+                const uint32_t q4 = quant4(vq[2 * k + h][0], vq[2 * k + h][1], vq[2 * k + h][2], vq[2 * k + h][3], e);
                 if (ok) *reinterpret_cast<uint32_t*>(p.Q8 + mrow * p.ldc + col + 16 * h) = q4;
               }
               if (ok && lg == 0) p.Q8s[mrow * (p.ldc / 32) + (n0 + wrow0) / 32 + k] = (uint8_t)e;
@@ -657,7 +650,7 @@ __global__ void __launch_bounds__(512) gemm_xs8_kernel(MxArgs p, int nc) {
           qv = u32x2{__float_as_uint(v[0] + v[1] + v[2] + v[3]), __float_as_uint(v[4] + v[5] + v[6] + v[7])};
         } else {
           e = mx_exp(__uint_as_float(lg_max_abs_bits(v)));
-          qv = quant8(v, exp2i(e));
+          qv = quant8(v, e);
         }
         const int col = 32 * t;                                   // first h column of the block
         uint8_t* c8 = p.C8 + orow[mb] + (col + 4 * lg);

@@ -429,7 +429,7 @@ __global__ void __launch_bounds__(kRpThreads, 1) gemm_rp_kernel(RpArgs p) {
           const float b2 = __uint_as_float(h1 << 16), b3 = __uint_as_float(h1 & 0xffff0000u);
           const float am = rp_max8(fmaxf(fmaxf(fabsf(b0), fabsf(b1)), fmaxf(fabsf(b2), fabsf(b3))));
           const int e = mx_exp(am);
-          const uint32_t q4 = quant4(b0, b1, b2, b3, exp2i(e));
+          const uint32_t q4 = quant4(b0, b1, b2, b3, e);
           ssq = fmaf(b3, b3, fmaf(b2, b2, fmaf(b1, b1, fmaf(b0, b0, ssq))));
           if (ok) {
             *reinterpret_cast<uint32_t*>(p.C8 + o) = q4;

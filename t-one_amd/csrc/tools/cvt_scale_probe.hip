@@ -17,7 +17,8 @@ __global__ void probe(const float* x, unsigned* out, int n) {
   const int e = tone::mx_exp(am);
   const float inv = tone::exp2i(e);                                  // 2^(127 - E), E = e biased
   const float sc = __uint_as_float((uint32_t)(e) << 23);            // 2^(e - 127): the block scale
-  const unsigned ref = tone::quant4(a, b, 0.f, 0.f, inv) & 0xffff;
+  // (a): the round-3..5 software path (the library now converts with the scaled instruction, common.h mx_cvt2)
+  const unsigned ref = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(tone::sat_e4m3(a * inv), tone::sat_e4m3(b * inv), 0, false) & 0xffff;
   const float lim = 448.f * sc;
   const float ca = __builtin_elementwise_minimum(__builtin_elementwise_maximum(a, -lim), lim);
   const float cb = __builtin_elementwise_minimum(__builtin_elementwise_maximum(b, -lim), lim);

@@ -425,13 +425,14 @@ np.savez(sys.argv[1], **out)
 
 def mx_quant_ref(xb: np.ndarray):
     """quant_mx_kernel (gemm_mx.hip) restated on the host for a bf16 [M][384] operand (raw bits): per 32-column block
-    E = clamp(biased exponent of max |v| - 8, 0, 254), values v * 2^(127 - E) clamped to +-448 and rounded to OCP e4m3
-    (round to nearest even, torch's float8_e4m3fn cast), and the row's sum of squares."""
+    E = clamp(biased exponent of max |v| - 7, 1, 254) (round 6: one binade of headroom, common.h mx_exp), values
+    v * 2^(127 - E) (all below 256, so the +-448 clamp never acts) rounded to OCP e4m3 (round to nearest even, torch's
+    float8_e4m3fn cast), and the row's sum of squares."""
     import torch
     m = xb.shape[0]
     v = (xb.astype(np.uint32) << 16).view(np.float32).reshape(m, 12, 32)
     amax = np.abs(v).max(axis=2)
-    e = np.clip(((amax.view(np.uint32) >> 23) & 0xFF).astype(np.int64) - 8, 0, 254)
+    e = np.clip(((amax.view(np.uint32) >> 23) & 0xFF).astype(np.int64) - 7, 1, 254)
     inv = ((254 - e).astype(np.uint32) << 23).view(np.float32)
     y = np.clip(v * inv[..., None], np.float32(-448), np.float32(448)).astype(np.float32)
     q = torch.from_numpy(y.reshape(m, 384)).to(torch.float8_e4m3fn).view(torch.uint8).numpy()
