@@ -1,18 +1,21 @@
-// fp32 mode (BASELINE config 2): the N = 384 projections of the small-M layers (attn-out, pw2, FFN down at M = B T =
-// 1280 / 2560) with the operands read straight into registers -- no LDS staging at all.
+// fp32 mode (BASELINE config 2): the N = 384 projections of the small-M layers (attn-out, pw2, FFN down and the
+// reduction's 1x1 at M = B T = 65 .. 4096) and pw1 with the operands read straight into registers -- no LDS staging of
+// operands at all.
 //
 // gemm_x3 stages W's three bf16 planes and the fp32 X rows through an LDS-DMA ring paced by workgroup barriers; at
 // these shapes a launch is 240-480 workgroups of a few K-steps each and that fill (~30-40 GB/s per CU) bounds it,
 // while the XCD's L2 serves plain vector loads at several times that rate (MI355X_MICROARCH.md, L2 ~34.5 TB/s).
-// Here each wave owns one 32 x 32 output tile (or a 1/WK share of its K range) and loads, per pair of 16-deep K-steps,
-// its X fragment (lane l: row m0 + (l & 31), 8 fp32 at K offset 8 (l >> 5) of each step, 4 x 16 B) and its W fragments
-// (lane l: row n0 + (l & 31) of each bf16 plane, 8 values of each step, 6 x 16 B) D pairs ahead of their use, both
-// fragment-packed (common.h xpk_off / wpk_off: each load instruction reads 1 KiB contiguous; row-major X, 32 row
-// segments per instruction, measured 1.5-2x slower: profiles/r06_d3_probe.jsonl); X is split
-// into its three bf16 terms in registers (split3, as gemm_x3) and each K-step takes gemm_x3's six products in gemm_x3's
-// order (small terms first), so the arithmetic is gemm_x3's.  W (the 884 KiB of planes of a 384 x 384 layer) stays
-// L2-resident; the workgroups that share X rows are dealt to one XCD.  With WK > 1 the K range is split over the
-// workgroup's waves and the partials are added in LDS in a fixed order.  The epilogue is gemm_x3's (tile_epilogue).
+// gemm_d3: each wave owns one 32 x 32 output tile (or a 1/WK share of its K range) and loads, per pair of 16-deep
+// K-steps, its X fragment (lane l: row m0 + (l & 31), 8 fp32 at K offset 8 (l >> 5) of each step, 4 x 16 B) and its W
+// fragments (lane l: row n0 + (l & 31) of each bf16 plane, 8 values of each step, 6 x 16 B) D pairs ahead of their use,
+// both fragment-packed (common.h xpk_off / wpk_off: each load instruction reads 1 KiB contiguous; row-major X, 32 row
+// segments per instruction, measured 1.5-2x slower: profiles/r06_d3_probe.jsonl); X is split into its three bf16 terms
+// in registers (split3, as gemm_x3) and each K-step takes gemm_x3's six products in gemm_x3's order (small terms
+// first), so the arithmetic is gemm_x3's.  W (the 884 KiB of planes of a 384 x 384 layer) stays L2-resident; the
+// workgroups that share X rows are dealt to one XCD.  With WK > 1 the K range is split over the workgroup's waves and
+// the partials are added in LDS in a fixed order.  The epilogue is gemm_x3's (tile_epilogue), including the optional
+// packed copy of C (GemmArgs::CP) that pw1 reads.
+// gemm_d3n: the same per-wave stream with NT W tiles per wave and the folded-norm row factor (pw1's GLU).
 #include <cstdlib>
 
 #include "common.h"
@@ -310,8 +313,9 @@ hipError_t gemm_d3n(const GemmArgs& a, int epi, int variant, hipStream_t st) {
       a.ldc % 4 != 0 || a.M <= 0 || (a.a_packed && a.lda != a.K))
     return hipErrorInvalidValue;
   // by shape (scripts/d3n_sweep.sh, profiles/r06_d3n_packed_sweep.jsonl, A packed, K = 384; in the step only pw1
-  // gains, session.hip): four W tiles per wave over four row blocks (3) for FFN up (M = 2560 / 1280: 43.2 / 23.8 vs 49.0 / 26.9 us on gemm_x3) and q|k|v at M >= 2048 (21.4 vs
-  // 24.9); two (2) for pw1 (14.6 / 13.0 vs 17.2 / 14.8) and the rest (q|k|v at 1280: 13.7 vs 15.7)
+  // gains, session.hip): four W tiles per wave over four row blocks (3) for FFN up (M = 2560 / 1280: 43.2 / 23.8 vs
+  // 49.0 / 26.9 us on gemm_x3) and q|k|v at M >= 2048 (21.4 vs 24.9); two (2) for pw1 (14.6 / 13.0 vs 17.2 / 14.8) and
+  // the rest (q|k|v at 1280: 13.7 vs 15.7)
   if (variant < 0) variant = (epi == EPI_SWIGLU || (a.N >= 1024 && a.M >= 2048)) ? 3 : 2;
   switch (variant) {   // the sweep's other arrangements (2 x 2 / 1 x 4 waves) were slower on every shape
     case 2: return launch_d3n<4, 1, 2, 3>(a, epi, st);
