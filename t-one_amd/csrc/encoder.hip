@@ -163,11 +163,28 @@ __global__ void __launch_bounds__(256) kv_assemble_ring_kernel(const void* __res
       store_act<OBF>(kv, ((int64_t)b * TK + S + i) * kD + c, y[q][e]);
     }
   }
-  // cached rows: ring frames 30 - S .. 29
-  for (int i = tid; i < S * kD; i += 256) {
-    const int j = i / kD, c = i % kD;
-    const int fr = ph + kMhsaS - S + j;
-    store_act<OBF>(kv, ((int64_t)b * TK + j) * kD + c, __half2float(rg[(int64_t)(fr % kMhsaS) * kD + c]));
+  // cached rows: ring frames 30 - S .. 29, eight channels per thread (ring rows and kv rows are 16-byte aligned)
+  for (int i = tid; i < S * (kD / 8); i += 256) {
+    const int j = i / (kD / 8), c = (i % (kD / 8)) * 8;
+    const int fr = (ph + kMhsaS - S + j) % kMhsaS;
+    const uint4 h = *reinterpret_cast<const uint4*>(rg + (int64_t)fr * kD + c);
+    const __half* hv = reinterpret_cast<const __half*>(&h);
+    const int64_t o = ((int64_t)b * TK + j) * kD + c;
+    if constexpr (OBF) {
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 lo = (__bf16)__half2float(hv[2 * e]), hi = (__bf16)__half2float(hv[2 * e + 1]);
+        w[e] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+      }
+      *reinterpret_cast<uint4*>(static_cast<uint16_t*>(kv) + o) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      float* d = static_cast<float*>(kv) + o;
+      *reinterpret_cast<float4*>(d) = make_float4(__half2float(hv[0]), __half2float(hv[1]), __half2float(hv[2]),
+                                                  __half2float(hv[3]));
+      *reinterpret_cast<float4*>(d + 4) = make_float4(__half2float(hv[4]), __half2float(hv[5]), __half2float(hv[6]),
+                                                      __half2float(hv[7]));
+    }
   }
   __syncthreads();   // every ring read of this stream is done before its oldest rows are overwritten
 #pragma unroll
