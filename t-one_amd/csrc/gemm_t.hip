@@ -505,7 +505,14 @@ __global__ void __launch_bounds__(TL::WN * TL::WM * TL::WK * 64) gemm_x3_kernel(
   const int lr = lane & 31, lh = lane >> 5;
   const int ntn = p.N / BNW;
   int m0, n0;
-  if ((ntn & 7) == 0) {
+  const int ntm = gridDim.x / ntn;
+  if (p.xcd_mn && (ntn & 3) == 0 && (ntm & 1) == 0) {
+    // XCDs as 2 (M halves) x 4 (N quarters): each XCD's L2 takes half of X and a quarter of the W planes (FFN up at
+    // M = 2560: 15.7 + 14.2 MB of fills over the chip instead of 31.5 + 7.1 with the N-only split below)
+    const int xcd = blockIdx.x & 7, li = blockIdx.x >> 3, nq = ntn >> 2, mh = ntm >> 1;
+    m0 = ((xcd >> 2) * mh + li / nq) * BMX;
+    n0 = ((xcd & 3) * nq + li % nq) * BNW;
+  } else if ((ntn & 7) == 0) {
     // large W (FFN up: 7 MB of planes > one XCD's 4 MB L2): XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8)
     // for every M-tile, so each W plane row is fetched into one L2 only and the X tile is reused
     // by the XCD's N-tiles back to back
@@ -718,6 +725,7 @@ hipError_t launch_x3(const GemmArgs& a0, hipStream_t st) {
   // static priority for waves NW/2..: fp32 B = 256 step 3.616 -> 3.583 ms, FFN down 897 -> 871 us
   // (profiles/r02_ab_x3_prio.jsonl)
   a.dbg |= 64;
+  a.xcd_mn = knobs().x3_xcd;
   const dim3 tiles((a.N / TL::BNW) * ((a.M + TL::BMX - 1) / TL::BMX), a.k_split ? a.K / a.k_split : 1);
   const dim3 block(TL::WN * TL::WM * TL::WK * 64);
   if (a.a_plane) {

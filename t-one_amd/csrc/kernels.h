@@ -21,6 +21,8 @@ struct Knobs {
   int ring_nt;         // TONE_RING_NT=0: dwconv_ring reads / writes the ring rows through the caches (bit-identical)
   int d3x;             // TONE_D3X=0: fp32 pw1 on gemm_x3 instead of gemm_d3n over the packed copy of the residual rows that
                        // attn-out writes (last-bit changes: the row factor's squares added in another order)
+  int x3_xcd;          // TONE_X3_XCD=0: gemm_x3 tiles dealt to XCDs by N only (each L2 fills all of X) instead of 2 M halves
+                       // x 4 N quarters (bit-identical)
   int d3;              // TONE_D3=0: fp32 N = 384 projections at small M on gemm_x3 instead of gemm_d3 (last-bit changes:
                        // the K-split partials are added in another order)
 };
@@ -74,6 +76,7 @@ struct GemmArgs {
   uint8_t* C8s;       // ... E8M0 [M][ldc / 32] ...
   float* ss8;         // ... and the rows' sum-of-squares slab [M][kSsSlots] (common.h)
   int order_n;        // bf16 LDS-DMA kernel: XCD x owns N-tiles [x*ntn/8, (x+1)*ntn/8) (large W)
+  int xcd_mn;         // gemm_x3: XCDs as 2 M halves x 4 N quarters of the tile grid (set by the launcher)
   int nt_store;       // non-temporal epilogue stores
   int dbg;            // microbenchmark only: 1 = no epilogue, 4 = no K loop
   const uint16_t* W3; // fp32 mode: W split into three bf16 planes [3][N][K] (gemm_x3), or nullptr
