@@ -163,6 +163,18 @@ def test_fp32_d3n_rowscale_matches_reference(M, N, epi, cpack):
     assert r["max_rel_err"] < 2e-5, r
 
 
+# gemm_x3's two tile-to-XCD deals (TONE_X3_XCD: 2 M halves x 4 N quarters, the default, where the tile grid allows it;
+# else the N-only split): every tile computed once and correctly under both (a deal that dropped or doubled a tile shows
+# as a wrong block), at the fp32 step's FFN up / q|k|v heights -- M = 3328 / 1536 have an odd M-tile count and take the
+# N-only split either way
+@pytest.mark.parametrize("M", [2560, 1280, 3328, 1536])
+@pytest.mark.parametrize("N,epi", [(3072, 2), (1152, 0)])
+def test_fp32_x3_xcd_deals_match_reference(M, N, epi):
+    _gpu()
+    r = [_run(M, 384, N, epi, -2, {"FULLF32": 1, "NOC2": 1, "ROWSCALE": 1, "TONE_X3_XCD": x}) for x in (0, 1)]
+    assert all(v["max_rel_err"] < 2e-5 for v in r) and r[0]["max_rel_err"] == r[1]["max_rel_err"], r
+
+
 # ... and the producer side of FFN down's packed A: the fp32 SwiGLU epilogue (gemm_x3) writing h fragment-packed, read
 # back through the inverse map
 @pytest.mark.parametrize("M", [2560, 1280, 3328, 1536, 640, 100])
