@@ -820,6 +820,104 @@ __global__ void __launch_bounds__(256) head_kernel(const void* __restrict__ x, c
   }
 }
 
+// The same on the exact-fp32 MFMA (v_mfma_f32_32x32x2_f32): head_kernel above reads its W quarter from LDS with the 16
+// row groups of a wave on the same four addresses, so the LDS pipe (1 KiB per wave-wide 16-byte read) bounds it at
+// ~3400 FMAs per lane on 40 CUs at M = 2560.  Here a workgroup owns 32 rows, its four waves a quarter of K (96) each;
+// lane (r = l & 31, h = l >> 5) loads row m0 + r and vocab rows r, r + 32 (zero past 34) at k = kq + 16 s + 8 h .. + 7
+// straight from L2 (W is 53 KB), MFMA e of step s takes element e -- A and B over the same k.  The quarters are added
+// through LDS in wave order, the 32 x 35 logit tile goes through LDS to one lane per row for the log-softmax / greedy /
+// speech-flag epilogue (head_kernel's formulas), and the block's 32 contiguous logprob rows leave as one coalesced run.
+typedef float f32x16h_t __attribute__((ext_vector_type(16)));
+template <bool R16>
+__global__ void __launch_bounds__(256) head_mfma_kernel(const void* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, float* __restrict__ logp,
+                                                        int32_t* __restrict__ frame_info, int rows) {
+  __shared__ float red[3][2][16][64];                // quarters 1..3 of the two 32-column vocab tiles
+  __shared__ float lg[32 * kVocab];                  // [row][v] logits, then logprobs (row stride 35: conflict-free)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.x * 32, kq = wid * kHeadQ;
+  const int64_t xr = (int64_t)min(m0 + r, rows - 1) * kD + kq + 8 * h;
+  constexpr int kS = kHeadQ / 16;                    // 6 steps of 16 k
+  f32x4_t xv[kS][2], wv[kS][2][2];
+#pragma unroll
+  for (int s = 0; s < kS; ++s) {
+    xv[s][0] = load_res4(x, xr + 16 * s, R16);
+    xv[s][1] = load_res4(x, xr + 16 * s + 4, R16);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int v = r + 32 * t;
+      const f32x4_t* wp = reinterpret_cast<const f32x4_t*>(w + (int64_t)min(v, kVocab - 1) * kD + kq + 8 * h + 16 * s);
+      const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+      wv[s][t][0] = v < kVocab ? wp[0] : z;
+      wv[s][t][1] = v < kVocab ? wp[1] : z;
+    }
+  }
+  f32x16h_t acc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+  for (int s = 0; s < kS; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[s][e >> 2][e & 3], wv[s][t][e >> 2][e & 3], acc[t], 0, 0, 0);
+  if (wid > 0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[wid - 1][t][i][lane] = acc[t][i];
+  }
+  __syncthreads();
+  if (wid > 0) return;
+  // D tile (row, vocab): register i of lane l holds row 8 (i >> 2) + 4 h + (i & 3), column r (+ 32 t)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int v = r + 32 * t;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float a = acc[t][i];
+      a += red[0][t][i][lane];
+      a += red[1][t][i][lane];
+      a += red[2][t][i][lane];
+      if (v < kVocab) lg[(8 * (i >> 2) + 4 * h + (i & 3)) * kVocab + v] = a + bias[v];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < 32) {   // lane = row of the block
+    float* z = lg + lane * kVocab;
+    float m = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < kVocab; ++v) m = fmaxf(m, z[v]);
+    float se = 0.f;
+#pragma unroll
+    for (int v = 0; v < kVocab; ++v) se += expf(z[v] - m);
+    const float lse = logf(se);
+    float best = -INFINITY;
+    int tok = 0;
+#pragma unroll
+    for (int v = 0; v < kVocab; ++v) {
+      const float l = z[v] - m - lse;
+      z[v] = l;
+      if (l > best) { best = l; tok = v; }
+    }
+    if (frame_info && m0 + lane < rows) {
+      const float sil = expf(z[kVocab - 2]) + expf(z[kVocab - 1]);
+      frame_info[m0 + lane] = tok | ((sil <= kSilenceThreshold) ? 256 : 0);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int n = min(32, rows - m0) * kVocab;         // the block's rows are contiguous in logp
+  float* dst = logp + (int64_t)m0 * kVocab;
+  for (int i = lane; i < n; i += 64) dst[i] = lg[i];
+}
+
 // The same for a few rows (the drop-in's B = 1 .. 6 streams): one wave per row, lane l owns k = l + 64 i (six k), W
 // read straight from L2 (no LDS staging, which the 256-row blocks amortise), the 35 partial sums combined by a
 // six-step xor butterfly; then the same log-softmax / greedy / speech-flag epilogue.
@@ -942,6 +1040,11 @@ hipError_t launch_head(const void* x, const float* w, const float* b, float* log
   if (rows <= 64) {
     if (r16) hipLaunchKernelGGL(head_rows_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
     else hipLaunchKernelGGL(head_rows_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
+    return hipGetLastError();
+  }
+  if (knobs().head_mfma) {
+    if (r16) hipLaunchKernelGGL(head_mfma_kernel<true>, dim3((rows + 31) / 32), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
+    else hipLaunchKernelGGL(head_mfma_kernel<false>, dim3((rows + 31) / 32), dim3(256), 0, st, x, w, b, logp, frame_info, rows);
     return hipGetLastError();
   }
   if (r16) hipLaunchKernelGGL(head_kernel<true>, dim3((rows + 63) / 64), dim3(256), 0, st, x, w, b, logp, frame_info, rows);

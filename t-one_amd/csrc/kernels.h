@@ -23,6 +23,8 @@ struct Knobs {
                        // attn-out writes (last-bit changes: the row factor's squares added in another order)
   int x3_xcd;          // TONE_X3_XCD=0: gemm_x3 tiles dealt to XCDs by N only (each L2 fills all of X) instead of 2 M halves
                        // x 4 N quarters (bit-identical)
+  int head_mfma;       // TONE_HEAD_MFMA=0: the CTC head (rows > 64) on LDS-fed FMAs instead of the exact-fp32 MFMA (last-bit
+                       // changes: the logits' K quarters added in another order)
   int d3;              // TONE_D3=0: fp32 N = 384 projections at small M on gemm_x3 instead of gemm_d3 (last-bit changes:
                        // the K-split partials are added in another order)
 };

@@ -38,6 +38,7 @@ const Knobs& knobs() {
     r.d3x = env("TONE_D3X", 1) != 0;
     r.ring_nt = env("TONE_RING_NT", 1) != 0;
     r.x3_xcd = env("TONE_X3_XCD", 1) != 0;
+    r.head_mfma = env("TONE_HEAD_MFMA", 1) != 0;
     return r;
   }();
   return k;

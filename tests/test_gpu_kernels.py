@@ -356,10 +356,11 @@ def test_upsample_add_every_element(T, check, B, tol):
         assert r["outputs"]["xp"] < tol, r
 
 
-@pytest.mark.parametrize("check,rows", [("head_r16", 40960), ("head_r16", 20480), ("head", 2560), ("head", 60),
-                                        ("head", 10)])
+@pytest.mark.parametrize("check,rows", [("head_r16", 40960), ("head_r16", 20480), ("head_r16", 4097), ("head", 2560),
+                                        ("head", 2570), ("head", 65), ("head", 60), ("head", 10)])
 def test_head_every_element(check, rows):
-    """CTC head + log_softmax + the greedy token / speech flag (head_kernel, and head_rows_kernel at <= 64 rows)."""
+    """CTC head + log_softmax + the greedy token / speech flag (head_mfma_kernel / head_kernel, and head_rows_kernel at
+    <= 64 rows); row counts off the 32-row block included."""
     _gpu()
     r = _check(check, rows)
     assert r["outputs"]["logprobs"] < 5e-5 and r["outputs"]["frame_info_bad"] == 0, r
